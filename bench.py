@@ -1,0 +1,227 @@
+"""Throughput benchmark of the MI355X MicroRTS engine (BASELINE.json metric).
+
+One "step" = one env-step of every env: get_action_mask() + device random
+masked-action sampler (hello_world.py:27-64 semantics) + step(), exactly the
+per-step API traffic of the reference rollout loop.  Workload:
+16x16 basesWorkers, 8192 envs per GPU (4096 selfplay games, random vs random),
+max_steps 2000, auto-reset on, inputs already resident in HBM.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Each rank owns an independent contiguous shard of envs (no data-path
+collective: envs never interact); the only communication is the timing
+barrier and the max-over-ranks of the elapsed time.
+
+Rank 0 prints one JSON line.  `roofline` prices the dominant kernel with HIP
+events recorded around every launch of it in the timed region;
+`cpu_baseline` times the CPU restatement (oracle/, OpenMP over games) on a
+bounded sample of the same workload (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "microrts-py_amd"))
+
+METRIC = "env-steps/sec (whole node), 16x16 basesWorkers @8192 envs; bit-exact vs Java"
+MAP = "maps/16x16/basesWorkers16x16.xml"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs-per-gpu", type=int, default=8192)
+    ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true")
+    return ap.parse_args()
+
+
+def kernel_bytes(G, N, HW, P=29):
+    """Algorithmic bytes per launch.
+    masks: game state read (16 B/cell/game) + mask write (78*4 B/cell/env) + source write (4 B/cell/env).
+    step : game state read+write (32 B/cell/game) + source read (4 B/cell/env) + obs write (4P B/cell/env)
+           + raw reward (48 B/env) + done (6 B/env); action rows (56 B per acting unit) not counted."""
+    return {
+        "get_masks": G * HW * 16 + N * HW * (78 * 4 + 4),
+        "step": G * HW * 32 + N * HW * (4 + 4 * P) + N * (48 + 6),
+    }
+
+
+def run_gpu(args, rank, world, local_rank):
+    import numpy as np
+    import torch
+
+    from gym_microrts import _native
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    n = args.envs_per_gpu
+    env = MicroRTSGridModeVecEnv(num_selfplay_envs=n, num_bot_envs=0, max_steps=args.max_steps, map_paths=[MAP],
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, return_tensors=True)
+    hw = env.height * env.width
+    act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
+    lib = _native.lib()
+    # shard-specific seed: rank r's envs are global envs [r*n, (r+1)*n)
+    seed = (args.seed << 32) | rank
+    ev = {}
+
+    def one_step(s):
+        m = env.get_action_mask()
+        if env.kernel_events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        rc = lib.mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), n, hw, seed, s, act.data_ptr())
+        if env.kernel_events is not None:
+            e1.record()
+            env.kernel_events.setdefault("sample", []).append((e0, e1))
+        _native.check(rc, None, "sample")
+        return env.step(act)
+
+    env.reset()
+    for s in range(args.warmup):
+        one_step(s)
+    if not args.no_kernel_events:
+        env.kernel_events = ev
+    barrier(world, dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, args.warmup + args.steps):
+        obs, rew, done, infos = one_step(s)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world, dev)
+    elapsed = t1 - t0
+    flags = env.error_flags()
+    kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
+    G = env.num_envs // 2
+    return elapsed, kern, flags, env.height * env.width, G, env.num_envs
+
+
+def barrier(world, dev):
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(seconds, envs=512):
+    """The oracle (C restatement, OpenMP over games) on a bounded sample of the
+    same workload: 16x16 basesWorkers selfplay, random masked actions."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from oracle_py import OracleVecEnv, sample_actions
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    path = os.path.join(REPO, "microrts-py_amd", "gym_microrts", "microrts", MAP)
+    o = OracleVecEnv(envs, 0, [path], max_steps=2000)
+    o.reset()
+    for s in range(5):
+        o.step(sample_actions(o.get_action_mask(), 1, s))
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds or steps < 5:
+        m = o.get_action_mask()
+        o.step(sample_actions(m, 1, 5 + steps))
+        steps += 1
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/libmrts_oracle.so, {envs} selfplay envs x {steps} steps ({dt:.1f} s), 16x16 basesWorkers, "
+                      f"masks + sampler + step + obs encode, OMP_NUM_THREADS={threads}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    elapsed, kern, flags, hw, G, N = run_gpu(args, rank, world, local_rank)
+    dev = torch.device("cuda", local_rank)
+    elapsed_max = max_over_ranks(elapsed, world, dev)
+    total_env_steps = world * N * args.steps
+    value = total_env_steps / elapsed_max
+    out = None
+    if rank == 0:
+        kb = kernel_bytes(G, N, hw)
+        roof = None
+        kernels = {}
+        for k, ms in kern.items():
+            entry = {"avg_ms": ms}
+            if k in kb:
+                entry["gbs"] = kb[k] / (ms * 1e-3) / 1e9
+                entry["bytes"] = kb[k]
+            kernels[k] = entry
+        dom = max((k for k in kern if k in kb), key=lambda k: kern[k], default=None)
+        if dom:
+            achieved = kb[dom] / (kern[dom] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                    "avg_launch_ms": round(kern[dom], 4)}
+        env_step_bytes = hw * (4 * 29 + 312 + 56 + 32) + 64   # SURVEY.md §8d whole-step formula
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed_max / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {"workload": "16x16 basesWorkers selfplay, random masked actions (device Philox sampler), "
+                                   "get_action_mask+sample+step per env-step",
+                       "envs_per_gpu": N, "games_per_gpu": G, "map": MAP, "max_steps": args.max_steps,
+                       "obs": "float32 device tensor", "parallelism": f"env-shard x{world}"},
+            "roofline": roof,
+            "kernels": kernels,
+            "env_step_bytes": env_step_bytes,
+            "env_step_roofline_frac": round(value / world * env_step_bytes / (HBM_PEAK_GBS * 1e9), 4),
+            "engine_error_flags": flags,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

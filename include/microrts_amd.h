@@ -1,0 +1,122 @@
+/*
+ * microrts_amd.h -- C ABI of the MI355X-native vectorised MicroRTS engine
+ * (libmicrorts_amd.so).
+ *
+ * This is the drop-in replacement for the FFI boundary the reference crosses
+ * on every reset / step / get_action_mask: JPype -> Java
+ * tests.JNIGridnetVecClient (constructed at
+ * /root/reference/gym_microrts/envs/vec_env.py:259-271).  Plain pointers and
+ * sizes only; no torch types.  Device buffers are allocated by the caller
+ * (hipMalloc, or a torch tensor's data_ptr) and all work is enqueued on the
+ * caller's hipStream_t, passed as `void *stream` (NULL = default stream).
+ *
+ * Ownership (reference: JNI path copies, shared-mem path aliases,
+ * vec_env.py:1276-1283, 1331-1333): output buffers are written in place and
+ * stay valid until the next call that writes them.
+ *
+ * Errors: every call returns MRTS_OK (0) or a negative MRTS_E* code, and
+ * mrts_last_error() holds a message (the reference surfaces Java exceptions
+ * through JPype; callers invoke e.printStackTrace(), ppo_gridnet.py:477-479).
+ *
+ * Threading: a handle is not thread-safe; one handle per device per process
+ * (the reference runs one in-process JVM per process, vec_env.py:153-169).
+ */
+#ifndef MICRORTS_AMD_H
+#define MICRORTS_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRTS_OK 0
+#define MRTS_EINVAL (-1)
+#define MRTS_EIO (-2)
+#define MRTS_EHIP (-3)
+#define MRTS_ENOTIMPL (-4)
+#define MRTS_ESTATE (-5)
+
+/* Opponent ids for bot envs; names as in gym_microrts/microrts_ai.py:13-61. */
+#define MRTS_AI_PASSIVE 0
+#define MRTS_AI_WORKER_RUSH 1
+#define MRTS_AI_LIGHT_RUSH 2
+#define MRTS_AI_RANDOM_BIASED 3
+#define MRTS_AI_COAC 4
+
+#define MRTS_OBS_INT32 0
+#define MRTS_OBS_FLOAT32 1
+
+typedef struct mrts_vec mrts_vec;
+
+/* Arguments of JNIGridnetVecClient(num_selfplay, num_bot, max_steps, rfs,
+ * micrortsPath, mapPaths, ai2s, utt, partialObs) (vec_env.py:261-271).  The six
+ * reward functions and the default UnitTypeTable are fixed (vec_env.py:172-195). */
+typedef struct {
+    int32_t num_selfplay_envs;   /* even; envs 2k/2k+1 are players 0/1 of game k */
+    int32_t num_bot_envs;        /* envs num_selfplay + j play player 0 vs bot_ai[j] */
+    int32_t max_steps;           /* JNIGridnetVecClient.maxSteps                     */
+    int32_t partial_obs;         /* PartiallyObservableGameState (31 planes)         */
+    int32_t num_maps;            /* map table: all maps share one height x width     */
+    const char *const *map_paths;/* PhysicalGameState XML files (absolute paths)     */
+    const int32_t *game_map;     /* [num_games] index into map_paths, NULL -> 0      */
+    const int32_t *bot_ai;       /* [num_bot_envs] MRTS_AI_*, NULL -> passive        */
+    int32_t obs_dtype;           /* MRTS_OBS_INT32 (reference dtype) or FLOAT32      */
+} mrts_config;
+
+typedef struct {
+    int32_t height, width;
+    int32_t num_envs, num_games;
+    int32_t obs_planes;          /* 29, or 31 with partial obs                       */
+    int32_t mask_channels;       /* 78 (getMasks' 79 minus the source channel)       */
+    int32_t action_components;   /* 7                                                */
+    size_t workspace_bytes;      /* device bytes mrts_bind_workspace needs           */
+} mrts_info_t;
+
+/* new JNIGridnetVecClient(...): parses the map XMLs, validates the config. */
+int mrts_create(const mrts_config *cfg, mrts_vec **out);
+int mrts_info(const mrts_vec *h, mrts_info_t *info);
+/* Attach caller-owned device memory of mrts_info().workspace_bytes (game state
+ * + map templates) and upload the maps on `stream`. */
+int mrts_bind_workspace(mrts_vec *h, void *dev_workspace, void *stream);
+
+/* JNIGridnetVecClient.reset(players) (vec_env.py:279): every game back to its
+ * map; obs [N][H][W][planes] (int32 or float32 per obs_dtype). */
+int mrts_reset(mrts_vec *h, void *stream, void *obs);
+
+/* JNIGridnetVecClient.getMasks(0) (vec_env.py:1097): mask [N][H*W][78] int32
+ * (channels 1..78) and source [N][H*W] int32 (channel 0). */
+int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source);
+
+/* step_async + JNIGridnetVecClient.gameStep (vec_env.py:968-984, 1002):
+ * actions [N][H*W][7] int64 (device), source [N][H*W] int32 = the source
+ * channel of the last mrts_get_masks (selects the rows, vec_env.py:974).
+ * Outputs: obs, raw_reward [N][6] float64 (the six reward functions), done
+ * [N][6] uint8.  Finished games auto-reset (terminal reward/done reported). */
+int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source,
+              void *obs, double *raw_reward, uint8_t *done);
+
+/* Map cycling (vec_env.py:1038-1056): reset `count` games (host arrays) onto
+ * the given map indices and rewrite their envs' obs. */
+int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);
+
+/* Random masked action sampler of hello_world.py:27-64 on the device
+ * (Philox4x32-10 keyed by seed, counter = (cell, env, step)). */
+int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int32_t hw, uint64_t seed,
+                        uint32_t step, int64_t *actions);
+
+/* Engine invariant violations recorded on the device (OR over games). */
+int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out);
+
+/* UnitTypeTable JSON as rts.units.UnitTypeTable.toJSON / sendUTT()
+ * (vec_env.py:276).  Valid for the lifetime of the handle. */
+const char *mrts_utt_json(const mrts_vec *h);
+
+const char *mrts_last_error(const mrts_vec *h);
+void mrts_destroy(mrts_vec *h);
+const char *mrts_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

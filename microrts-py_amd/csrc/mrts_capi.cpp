@@ -1,0 +1,372 @@
+// mrts_capi.cpp -- C ABI of libmicrorts_amd.so (include/microrts_amd.h).
+//
+// Host side of the replacement for tests.JNIGridnetVecClient
+// (/root/reference/gym_microrts/envs/vec_env.py:256-276): config validation,
+// PhysicalGameState XML loading into device map templates, workspace carving
+// and kernel dispatch.  No torch types cross this boundary.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "microrts_amd.h"
+#include "mrts_engine.h"
+#include "mrts_layout.h"
+
+namespace {
+
+const char *kTypeNames[MRTS_NTYPES] = {"Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"};
+
+struct MapData {
+    int w = 0, h = 0;
+    std::vector<uint8_t> wall;
+    int res[2] = {0, 0};
+    std::vector<int4> cells;  // template records (unit word, uid, 0, 0)
+    int nunits = 0;
+};
+
+std::string attr(const std::string &tag, const char *name) {
+    std::string key = std::string(" ") + name + "=\"";
+    size_t p = tag.find(key);
+    if (p == std::string::npos) return std::string();
+    p += key.size();
+    size_t q = tag.find('"', p);
+    return q == std::string::npos ? std::string() : tag.substr(p, q - p);
+}
+
+bool to_int(const std::string &s, int *out) {
+    if (s.empty()) return false;
+    char *end = nullptr;
+    long v = std::strtol(s.c_str(), &end, 10);
+    if (*end) return false;
+    *out = (int)v;
+    return true;
+}
+
+uint32_t unit_word(int type, int owner, int hp, int res) {
+    return (uint32_t)(type + 1) | ((uint32_t)(owner + 1) << 4) | ((uint32_t)hp << 6) | ((uint32_t)res << 16);
+}
+
+// rts.PhysicalGameState.load (XML form of /root/reference/PCG/maps/wall-1:1-16)
+bool load_map(const char *path, MapData *m, std::string *err) {
+    std::ifstream f(path);
+    if (!f) { *err = std::string("cannot open map ") + path; return false; }
+    std::stringstream ss;
+    ss << f.rdbuf();
+    std::string x = ss.str();
+    size_t root = x.find("<rts.PhysicalGameState");
+    if (root == std::string::npos) { *err = std::string("not a PhysicalGameState XML: ") + path; return false; }
+    std::string rtag = x.substr(root, x.find('>', root) - root);
+    if (!to_int(attr(rtag, "width"), &m->w) || !to_int(attr(rtag, "height"), &m->h) || m->w <= 0 || m->h <= 0) {
+        *err = std::string("bad width/height in ") + path;
+        return false;
+    }
+    const int HW = m->w * m->h;
+    if (HW > MRTS_MAX_HW) { *err = "map larger than MRTS_MAX_HW cells"; return false; }
+    size_t t0 = x.find("<terrain>"), t1 = x.find("</terrain>");
+    if (t0 == std::string::npos || t1 == std::string::npos) { *err = "missing <terrain>"; return false; }
+    std::string terr;
+    for (size_t i = t0 + 9; i < t1; i++)
+        if (x[i] == '0' || x[i] == '1') terr.push_back(x[i]);
+    if ((int)terr.size() != HW) { *err = std::string("terrain length mismatch in ") + path; return false; }
+    m->wall.assign(HW, 0);
+    for (int i = 0; i < HW; i++) m->wall[i] = terr[i] == '1';
+    size_t pos = 0;
+    while ((pos = x.find("<rts.Player ", pos)) != std::string::npos) {
+        std::string tag = x.substr(pos, x.find('>', pos) - pos);
+        int id = -1, r = 0;
+        if (!to_int(attr(tag, "ID"), &id) || !to_int(attr(tag, "resources"), &r) || id < 0 || id > 1) {
+            *err = "bad <rts.Player>";
+            return false;
+        }
+        m->res[id] = r;
+        pos += 12;
+    }
+    m->cells.assign(HW, make_int4(0, 0, 0, 0));
+    pos = 0;
+    int idx = 0;
+    while ((pos = x.find("<rts.units.Unit ", pos)) != std::string::npos) {
+        std::string tag = x.substr(pos, x.find('>', pos) - pos);
+        std::string tn = attr(tag, "type");
+        int type = -1;
+        for (int k = 0; k < MRTS_NTYPES; k++)
+            if (tn == kTypeNames[k]) type = k;
+        int player, ux, uy, ur, hp;
+        if (type < 0 || !to_int(attr(tag, "player"), &player) || !to_int(attr(tag, "x"), &ux) ||
+            !to_int(attr(tag, "y"), &uy) || !to_int(attr(tag, "resources"), &ur) || !to_int(attr(tag, "hitpoints"), &hp)) {
+            *err = std::string("bad <rts.units.Unit> in ") + path;
+            return false;
+        }
+        if (ux < 0 || uy < 0 || ux >= m->w || uy >= m->h || player < -1 || player > 1 || hp < 1 || hp > 1023 ||
+            ur < 0 || ur > 65535) {
+            *err = std::string("unit out of range in ") + path;
+            return false;
+        }
+        int c = uy * m->w + ux;
+        if (m->cells[c].x != 0) { *err = std::string("two units in one cell in ") + path; return false; }
+        m->cells[c] = make_int4((int)unit_word(type, player, hp, ur), idx++, 0, 0);
+        pos += 16;
+    }
+    m->nunits = idx;
+    return true;
+}
+
+std::string utt_json() {
+    // rts.units.UnitTypeTable.toJSON of UnitTypeTable() (VERSION_ORIGINAL)
+    struct T { const char *n; int cost, hp, mind, maxd, range, pt, mt, at, ht, rt, ha, sight; int res, stock, harv, move, atk; const char *prod, *by; };
+    static const T ts[] = {
+        {"Resource", 1, 1, 1, 1, 1, 10, 10, 10, 10, 10, 1, 0, 1, 0, 0, 0, 0, "", ""},
+        {"Base", 10, 10, 1, 1, 1, 250, 10, 10, 10, 10, 1, 5, 0, 1, 0, 0, 0, "\"Worker\"", "\"Worker\""},
+        {"Barracks", 5, 4, 1, 1, 1, 200, 10, 10, 10, 10, 1, 3, 0, 0, 0, 0, 0, "\"Light\", \"Heavy\", \"Ranged\"", "\"Worker\""},
+        {"Worker", 1, 1, 1, 1, 1, 50, 10, 5, 20, 10, 1, 3, 0, 0, 1, 1, 1, "\"Base\", \"Barracks\"", "\"Base\""},
+        {"Light", 2, 4, 2, 2, 1, 80, 8, 5, 10, 10, 1, 2, 0, 0, 0, 1, 1, "", "\"Barracks\""},
+        {"Heavy", 2, 4, 4, 4, 1, 120, 12, 5, 10, 10, 1, 2, 0, 0, 0, 1, 1, "", "\"Barracks\""},
+        {"Ranged", 2, 1, 1, 1, 3, 100, 10, 5, 10, 10, 1, 3, 0, 0, 0, 1, 1, "", "\"Barracks\""},
+    };
+    std::string s = "{\"moveConflictResolutionStrategy\":3,\"unitTypes\":[";
+    char buf[1024];
+    for (int i = 0; i < MRTS_NTYPES; i++) {
+        const T &t = ts[i];
+        std::snprintf(buf, sizeof buf,
+                      "%s{\"ID\":%d, \"name\":\"%s\", \"cost\":%d, \"hp\":%d, \"minDamage\":%d, \"maxDamage\":%d, "
+                      "\"attackRange\":%d, \"produceTime\":%d, \"moveTime\":%d, \"attackTime\":%d, \"harvestTime\":%d, "
+                      "\"returnTime\":%d, \"harvestAmount\":%d, \"sightRadius\":%d, \"isResource\":%s, \"isStockpile\":%s, "
+                      "\"canHarvest\":%s, \"canMove\":%s, \"canAttack\":%s, \"produces\":[%s], \"producedBy\":[%s]}",
+                      i ? ", " : "", i, t.n, t.cost, t.hp, t.mind, t.maxd, t.range, t.pt, t.mt, t.at, t.ht, t.rt, t.ha,
+                      t.sight, t.res ? "true" : "false", t.stock ? "true" : "false", t.harv ? "true" : "false",
+                      t.move ? "true" : "false", t.atk ? "true" : "false", t.prod, t.by);
+        s += buf;
+    }
+    s += "]}";
+    return s;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct mrts_vec {
+    int nsp = 0, nbot = 0, ngames = 0, nenvs = 0, max_steps = 0, partial_obs = 0, obs_float = 0;
+    int W = 0, H = 0, HW = 0;
+    std::vector<MapData> maps;
+    std::vector<int32_t> game_map;
+    std::vector<int32_t> bot_ai;
+    // workspace carving
+    size_t off_cells = 0, off_genv = 0, off_mcells = 0, off_mwall = 0, off_mscal = 0, off_scratch = 0, total = 0;
+    unsigned char *ws = nullptr;
+    std::vector<int32_t> scratch_host;
+    std::string err, utt;
+    EngineParams base{};
+};
+
+static int fail(mrts_vec *h, int code, const std::string &msg) {
+    if (h) h->err = msg;
+    return code;
+}
+static int hip_fail(mrts_vec *h, hipError_t e, const char *what) {
+    return fail(h, MRTS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+extern "C" {
+
+const char *mrts_version(void) { return "microrts_amd 0.1 (gfx950)"; }
+
+int mrts_create(const mrts_config *cfg, mrts_vec **out) {
+    if (!cfg || !out) return MRTS_EINVAL;
+    *out = nullptr;
+    mrts_vec *h = new mrts_vec();
+    h->utt = utt_json();
+    *out = h;
+    if (cfg->num_selfplay_envs < 0 || cfg->num_bot_envs < 0 || (cfg->num_selfplay_envs & 1))
+        return fail(h, MRTS_EINVAL, "num_selfplay_envs must be even and >= 0, num_bot_envs >= 0");
+    if (cfg->num_selfplay_envs + cfg->num_bot_envs <= 0) return fail(h, MRTS_EINVAL, "no envs");
+    if (cfg->max_steps <= 0 || cfg->max_steps >= MRTS_MAX_TIME)
+        return fail(h, MRTS_EINVAL, "max_steps must be in [1, 500000)");
+    if (cfg->partial_obs) return fail(h, MRTS_ENOTIMPL, "partial_obs is not implemented yet (DESIGN.md §8)");
+    if (cfg->num_maps <= 0 || !cfg->map_paths) return fail(h, MRTS_EINVAL, "no maps");
+    h->nsp = cfg->num_selfplay_envs;
+    h->nbot = cfg->num_bot_envs;
+    h->ngames = h->nsp / 2 + h->nbot;
+    h->nenvs = h->nsp + h->nbot;
+    h->max_steps = cfg->max_steps;
+    h->partial_obs = cfg->partial_obs;
+    h->obs_float = cfg->obs_dtype == MRTS_OBS_FLOAT32;
+    h->maps.resize(cfg->num_maps);
+    for (int i = 0; i < cfg->num_maps; i++) {
+        std::string e;
+        if (!load_map(cfg->map_paths[i], &h->maps[i], &e)) return fail(h, MRTS_EIO, e);
+        if (i > 0 && (h->maps[i].w != h->maps[0].w || h->maps[i].h != h->maps[0].h))
+            return fail(h, MRTS_EINVAL, "all maps of one vec env must share height x width (vec_env.py:149-150)");
+    }
+    h->W = h->maps[0].w;
+    h->H = h->maps[0].h;
+    h->HW = h->W * h->H;
+    if (mrts_engine_lds_bytes(h->HW, h->W) > 65536)
+        return fail(h, MRTS_ENOTIMPL, "map too large for one workgroup's LDS (max 24x24-class maps so far)");
+    h->game_map.assign(h->ngames, 0);
+    for (int g = 0; g < h->ngames; g++) {
+        int m = cfg->game_map ? cfg->game_map[g] : 0;
+        if (m < 0 || m >= cfg->num_maps) return fail(h, MRTS_EINVAL, "game_map index out of range");
+        h->game_map[g] = m;
+    }
+    h->bot_ai.assign(h->nbot, MRTS_AI_PASSIVE);
+    for (int j = 0; j < h->nbot; j++) {
+        int a = cfg->bot_ai ? cfg->bot_ai[j] : MRTS_AI_PASSIVE;
+        if (a != MRTS_AI_PASSIVE) return fail(h, MRTS_ENOTIMPL, "only passiveAI bots run on the device so far (DESIGN.md §8)");
+        h->bot_ai[j] = a;
+    }
+    size_t o = 0;
+    h->off_cells = o; o = align256(o + (size_t)h->ngames * h->HW * sizeof(int4));
+    h->off_genv = o; o = align256(o + (size_t)h->ngames * MRTS_GENV_WORDS * sizeof(int32_t));
+    h->off_mcells = o; o = align256(o + (size_t)cfg->num_maps * h->HW * sizeof(int4));
+    h->off_mwall = o; o = align256(o + (size_t)cfg->num_maps * h->HW);
+    h->off_mscal = o; o = align256(o + (size_t)cfg->num_maps * MRTS_MAP_SCALARS * sizeof(int32_t));
+    h->off_scratch = o; o = align256(o + (size_t)2 * h->ngames * sizeof(int32_t));
+    h->total = o;
+    h->err.clear();
+    return MRTS_OK;
+}
+
+int mrts_info(const mrts_vec *h, mrts_info_t *info) {
+    if (!h || !info || h->HW == 0) return MRTS_EINVAL;
+    info->height = h->H;
+    info->width = h->W;
+    info->num_envs = h->nenvs;
+    info->num_games = h->ngames;
+    info->obs_planes = h->partial_obs ? 31 : 29;
+    info->mask_channels = MRTS_MASK_CH;
+    info->action_components = 7;
+    info->workspace_bytes = h->total;
+    return MRTS_OK;
+}
+
+int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
+    if (!h || !dev || h->HW == 0) return fail(h, MRTS_EINVAL, "bind_workspace: bad handle or pointer");
+    if (((uintptr_t)dev & 255u) != 0) return fail(h, MRTS_EINVAL, "workspace must be 256-byte aligned");
+    hipStream_t s = (hipStream_t)stream;
+    h->ws = (unsigned char *)dev;
+    const int nm = (int)h->maps.size();
+    std::vector<int4> mc((size_t)nm * h->HW);
+    std::vector<uint8_t> mw((size_t)nm * h->HW);
+    std::vector<int32_t> ms((size_t)nm * MRTS_MAP_SCALARS, 0);
+    for (int i = 0; i < nm; i++) {
+        std::memcpy(&mc[(size_t)i * h->HW], h->maps[i].cells.data(), sizeof(int4) * h->HW);
+        std::memcpy(&mw[(size_t)i * h->HW], h->maps[i].wall.data(), h->HW);
+        ms[i * MRTS_MAP_SCALARS + MRTS_M_RES0] = h->maps[i].res[0];
+        ms[i * MRTS_MAP_SCALARS + MRTS_M_RES1] = h->maps[i].res[1];
+        ms[i * MRTS_MAP_SCALARS + MRTS_M_NUNITS] = h->maps[i].nunits;
+    }
+    std::vector<int32_t> genv((size_t)h->ngames * MRTS_GENV_WORDS, 0);
+    for (int g = 0; g < h->ngames; g++) genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP] = h->game_map[g];
+    hipError_t e;
+    if ((e = hipMemcpyAsync(h->ws + h->off_mcells, mc.data(), mc.size() * sizeof(int4), hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(h->ws + h->off_mwall, mw.data(), mw.size(), hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(h->ws + h->off_mscal, ms.data(), ms.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(h->ws + h->off_genv, genv.data(), genv.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) ||
+        (e = hipStreamSynchronize(s)))
+        return hip_fail(h, e, "bind_workspace upload");
+    EngineParams &p = h->base;
+    p = EngineParams{};
+    p.cells = (int4 *)(h->ws + h->off_cells);
+    p.genv = (int32_t *)(h->ws + h->off_genv);
+    p.map_cells = (const int4 *)(h->ws + h->off_mcells);
+    p.map_wall = (const uint8_t *)(h->ws + h->off_mwall);
+    p.map_scal = (const int32_t *)(h->ws + h->off_mscal);
+    p.G = h->ngames;
+    p.HW = h->HW;
+    p.W = h->W;
+    p.H = h->H;
+    p.nsp = h->nsp;
+    p.nsp_games = h->nsp / 2;
+    p.max_steps = h->max_steps;
+    p.obs_float = h->obs_float;
+    h->err.clear();
+    return MRTS_OK;
+}
+
+static bool bound(mrts_vec *h) { return h && h->ws; }
+
+int mrts_reset(mrts_vec *h, void *stream, void *obs) {
+    if (!bound(h) || !obs) return fail(h, MRTS_ESTATE, "reset: workspace not bound or obs null");
+    EngineParams p = h->base;
+    p.obs = obs;
+    hipError_t e = mrts_engine_reset(&p, (hipStream_t)stream, nullptr, nullptr, 0);
+    return e ? hip_fail(h, e, "reset launch") : MRTS_OK;
+}
+
+int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source) {
+    if (!bound(h) || !mask || !source) return fail(h, MRTS_ESTATE, "get_masks: workspace not bound or null output");
+    EngineParams p = h->base;
+    p.mask = mask;
+    p.src_out = source;
+    hipError_t e = mrts_engine_masks(&p, (hipStream_t)stream);
+    return e ? hip_fail(h, e, "masks launch") : MRTS_OK;
+}
+
+int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs, double *raw_reward,
+              uint8_t *done) {
+    if (!bound(h) || !actions || !source || !obs || !raw_reward || !done)
+        return fail(h, MRTS_ESTATE, "step: workspace not bound or null buffer");
+    EngineParams p = h->base;
+    p.actions = actions;
+    p.src = source;
+    p.obs = obs;
+    p.raw_reward = raw_reward;
+    p.done = done;
+    hipError_t e = mrts_engine_step(&p, (hipStream_t)stream);
+    return e ? hip_fail(h, e, "step launch") : MRTS_OK;
+}
+
+int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs) {
+    if (!bound(h) || !obs || count < 0 || count > h->ngames || (count && (!games || !maps)))
+        return fail(h, MRTS_EINVAL, "reset_games: bad arguments");
+    if (count == 0) return MRTS_OK;
+    for (int i = 0; i < count; i++) {
+        if (games[i] < 0 || games[i] >= h->ngames || maps[i] < 0 || maps[i] >= (int)h->maps.size())
+            return fail(h, MRTS_EINVAL, "reset_games: index out of range");
+        h->game_map[games[i]] = maps[i];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    h->scratch_host.assign(games, games + count);
+    h->scratch_host.insert(h->scratch_host.end(), maps, maps + count);
+    int32_t *dg = (int32_t *)(h->ws + h->off_scratch);
+    hipError_t e = hipMemcpyAsync(dg, h->scratch_host.data(), sizeof(int32_t) * 2 * count, hipMemcpyHostToDevice, s);
+    if (e) return hip_fail(h, e, "reset_games upload");
+    EngineParams p = h->base;
+    p.obs = obs;
+    e = mrts_engine_reset(&p, s, dg, dg + count, count);
+    if (e) return hip_fail(h, e, "reset_games launch");
+    // the host staging vector must outlive the copy
+    e = hipStreamSynchronize(s);
+    return e ? hip_fail(h, e, "reset_games sync") : MRTS_OK;
+}
+
+int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw, uint64_t seed, uint32_t step,
+                        int64_t *actions) {
+    if (!mask || !actions || n < 0 || hw <= 0) return MRTS_EINVAL;
+    return mrts_engine_sample(mask, n, hw, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
+}
+
+int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {
+    if (!bound(h) || !flags_out) return fail(h, MRTS_ESTATE, "error_flags: not bound");
+    std::vector<int32_t> genv((size_t)h->ngames * MRTS_GENV_WORDS);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemcpyAsync(genv.data(), h->ws + h->off_genv, genv.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (!e) e = hipStreamSynchronize(s);
+    if (e) return hip_fail(h, e, "error_flags readback");
+    int32_t f = 0;
+    for (int g = 0; g < h->ngames; g++) f |= genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_ERR];
+    *flags_out = f;
+    return MRTS_OK;
+}
+
+const char *mrts_utt_json(const mrts_vec *h) { return h ? h->utt.c_str() : ""; }
+const char *mrts_last_error(const mrts_vec *h) { return h ? h->err.c_str() : "null handle"; }
+void mrts_destroy(mrts_vec *h) { delete h; }
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+// mrts_engine.h -- internal launch interface between the C ABI (mrts_capi.cpp)
+// and the kernels (mrts_engine.hip).
+#ifndef MRTS_ENGINE_H
+#define MRTS_ENGINE_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct EngineParams {
+    int4 *cells;            // [G][HW]
+    int32_t *genv;          // [G][MRTS_GENV_WORDS]
+    const int4 *map_cells;  // [maps][HW]
+    const uint8_t *map_wall;// [maps][HW]
+    const int32_t *map_scal;// [maps][MRTS_MAP_SCALARS]
+    int G, HW, W, H;
+    int nsp, nsp_games, max_steps, obs_float;
+    const int64_t *actions; // [N][HW][7]
+    const int32_t *src;     // [N][HW]
+    void *obs;              // [N][HW][P]
+    double *raw_reward;     // [N][6]
+    uint8_t *done;          // [N][6]
+    int32_t *mask;          // [N][HW][78]
+    int32_t *src_out;       // [N][HW]
+};
+
+extern "C" {
+hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t *games, const int32_t *maps, int count);
+hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
+hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
+hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
+size_t mrts_engine_lds_bytes(int HW, int W);
+}
+#endif

@@ -1,0 +1,931 @@
+// mrts_engine.hip -- gfx950 kernels of the vectorised MicroRTS engine.
+//
+// Restates, on the device, the Java path behind MicroRTSGridModeVecEnv
+// (/root/reference/gym_microrts/envs/vec_env.py): JNIGridnetVecClient.reset
+// (vec_env.py:279), .gameStep (vec_env.py:1002: JNIAI action decode, issueSafe
+// p0/p1, GameState.cycle, the six ai.reward functions, auto-reset) and
+// .getMasks (vec_env.py:1097), plus the python-side one-hot encoder
+// _encode_obs (vec_env.py:311-321).  Rules: SURVEY.md Appendix A, DESIGN.md §4.
+//
+// Mapping: one workgroup per GAME, one lane per grid cell (16x16 -> 256 lanes),
+// the game's cell records staged in LDS.  Everything that is per-cell runs
+// lane-parallel (decode, legality, masks, readiness, one-hot); the parts of the
+// Java that are inherently ordered (PlayerAction consistency filter, issue()
+// conflict resolution, execution of ready actions in LinkedHashMap order) run
+// on lane 0 over compact ballot-built lists, which hold only the few units
+// that act this tick.  Outputs are written with 16-byte stores from compact
+// per-cell bit words in LDS (one-hot obs: 1 word/cell, mask: 3 words/cell).
+//
+// Integer work only: no MFMA, the kernels are HBM-bound on the obs/mask writes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mrts_engine.h"
+#include "mrts_layout.h"
+
+namespace mrts {
+
+// ---------------------------------------------------------------------------
+// rts.units.UnitTypeTable() -- VERSION_ORIGINAL (+ UnitType field defaults).
+enum { RESOURCE = 0, BASE, BARRACKS, WORKER, LIGHT, HEAVY, RANGED };
+enum { A_NONE = 0, A_MOVE, A_HARVEST, A_RETURN, A_PRODUCE, A_ATTACK };
+
+__device__ __forceinline__ int ut_cost(int t) { return t == BASE ? 10 : t == BARRACKS ? 5 : (t >= LIGHT ? 2 : 1); }
+__device__ __forceinline__ int ut_hp(int t) { return t == BASE ? 10 : (t == BARRACKS || t == LIGHT || t == HEAVY) ? 4 : 1; }
+__device__ __forceinline__ int ut_damage(int t) { return t == LIGHT ? 2 : t == HEAVY ? 4 : 1; }
+__device__ __forceinline__ int ut_range(int t) { return t == RANGED ? 3 : 1; }
+__device__ __forceinline__ int ut_produce_time(int t) {
+    return t == BASE ? 250 : t == BARRACKS ? 200 : t == WORKER ? 50 : t == LIGHT ? 80 : t == HEAVY ? 120 : t == RANGED ? 100 : 10;
+}
+__device__ __forceinline__ int ut_move_time(int t) { return t == LIGHT ? 8 : t == HEAVY ? 12 : 10; }
+__device__ __forceinline__ int ut_attack_time(int t) { return t >= WORKER ? 5 : 10; }
+__device__ __forceinline__ int ut_harvest_time(int t) { return t == WORKER ? 20 : 10; }
+__device__ __forceinline__ int ut_return_time(int) { return 10; }
+__device__ __forceinline__ int ut_harvest_amount(int) { return 1; }
+__device__ __forceinline__ bool ut_can_move(int t) { return t >= WORKER; }
+__device__ __forceinline__ bool ut_can_attack(int t) { return t >= WORKER; }
+__device__ __forceinline__ bool ut_can_harvest(int t) { return t == WORKER; }
+__device__ __forceinline__ bool ut_is_stockpile(int t) { return t == BASE; }
+// bitmask of produced unit types
+__device__ __forceinline__ int ut_produces(int t) {
+    return t == BASE ? (1 << WORKER) : t == BARRACKS ? ((1 << LIGHT) | (1 << HEAVY) | (1 << RANGED)) : t == WORKER ? ((1 << BASE) | (1 << BARRACKS)) : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Packed words (mrts_layout.h)
+__device__ __forceinline__ int u_type(uint32_t w) { return (int)(w & 15u) - 1; }
+__device__ __forceinline__ int u_owner(uint32_t w) { return (int)((w >> 4) & 3u) - 1; }
+__device__ __forceinline__ int u_hp(uint32_t w) { return (int)((w >> 6) & 1023u); }
+__device__ __forceinline__ int u_res(uint32_t w) { return (int)(w >> 16); }
+__device__ __forceinline__ uint32_t u_make(int type, int owner, int hp, int res) {
+    return (uint32_t)(type + 1) | ((uint32_t)(owner + 1) << 4) | ((uint32_t)hp << 6) | ((uint32_t)res << 16);
+}
+__device__ __forceinline__ uint32_t u_with_hp(uint32_t w, int hp) { return (w & ~(1023u << 6)) | ((uint32_t)hp << 6); }
+__device__ __forceinline__ uint32_t u_with_res(uint32_t w, int res) { return (w & 0xFFFFu) | ((uint32_t)res << 16); }
+
+// action code (12 bits): type | param << 3 | utype << 9 ; action word = code + 1 | (done + 1) << 12
+__device__ __forceinline__ int code_make(int type, int param, int utype) { return type | (param << 3) | (utype << 9); }
+__device__ __forceinline__ int code_type(int code) { return code & 7; }
+__device__ __forceinline__ int code_param(int code) { return (code >> 3) & 63; }
+__device__ __forceinline__ int code_utype(int code) { return (code >> 9) & 7; }
+__device__ __forceinline__ uint32_t act_make(int code, int done) { return (uint32_t)(code + 1) | ((uint32_t)(done + 1) << 12); }
+__device__ __forceinline__ int act_code(uint32_t a) { return (int)(a & 0xFFFu) - 1; }
+__device__ __forceinline__ int act_done(uint32_t a) { return (int)(a >> 12) - 1; }
+__device__ __forceinline__ uint32_t seq_make(int time, int player, int rank) {
+    return ((uint32_t)time << 13) | ((uint32_t)player << 12) | (uint32_t)rank;
+}
+__device__ __forceinline__ int seq_time(uint32_t s) { return (int)(s >> 13); }
+
+// UnitAction.ETA for a non-NONE code executed by a unit of type t
+__device__ __forceinline__ int eta_code(int code, int t) {
+    switch (code_type(code)) {
+    case A_MOVE: return ut_move_time(t);
+    case A_HARVEST: return ut_harvest_time(t);
+    case A_RETURN: return ut_return_time(t);
+    case A_PRODUCE: return ut_produce_time(code_utype(code));
+    case A_ATTACK: return ut_attack_time(t);
+    }
+    return 0;
+}
+
+__device__ __forceinline__ int dir_dx(int d) { return d == 1 ? 1 : d == 3 ? -1 : 0; }
+__device__ __forceinline__ int dir_dy(int d) { return d == 2 ? 1 : d == 0 ? -1 : 0; }
+
+struct Grid {
+    int W, H, HW;
+};
+
+// neighbour cell in direction d, or -1 when off the map
+__device__ __forceinline__ int nb_cell(const Grid& gd, int c, int d) {
+    int x = c % gd.W + dir_dx(d), y = c / gd.W + dir_dy(d);
+    return (x < 0 || y < 0 || x >= gd.W || y >= gd.H) ? -1 : y * gd.W + x;
+}
+
+// Unit.getUnitActions membership test (UnitAction.equals), i.e.
+// Unit.canExecuteAction for a decoded action code of the unit at cell c.
+__device__ bool legal_code(const Grid& gd, int c, int code, const uint32_t* s_unit, const uint8_t* s_wall, int res_player) {
+    uint32_t u = s_unit[c];
+    int t = u_type(u), owner = u_owner(u);
+    int type = code_type(code), param = code_param(code);
+    switch (type) {
+    case A_NONE: return true;
+    case A_MOVE: {
+        if (!ut_can_move(t)) return false;
+        int n = nb_cell(gd, c, param);
+        return n >= 0 && !s_wall[n] && s_unit[n] == 0;
+    }
+    case A_HARVEST: {
+        if (!ut_can_harvest(t) || u_res(u) != 0) return false;
+        int n = nb_cell(gd, c, param);
+        return n >= 0 && s_unit[n] != 0 && u_type(s_unit[n]) == RESOURCE;
+    }
+    case A_RETURN: {
+        if (!ut_can_harvest(t) || u_res(u) <= 0) return false;
+        int n = nb_cell(gd, c, param);
+        return n >= 0 && s_unit[n] != 0 && ut_is_stockpile(u_type(s_unit[n])) && u_owner(s_unit[n]) == owner;
+    }
+    case A_PRODUCE: {
+        int ut = code_utype(code);
+        if (!((ut_produces(t) >> ut) & 1) || res_player < ut_cost(ut)) return false;
+        int n = nb_cell(gd, c, param);
+        return n >= 0 && !s_wall[n] && s_unit[n] == 0;
+    }
+    case A_ATTACK: {
+        if (!ut_can_attack(t)) return false;
+        int dx = param % MRTS_ATTACK_GRID - MRTS_ATTACK_GRID / 2, dy = param / MRTS_ATTACK_GRID - MRTS_ATTACK_GRID / 2;
+        int r = ut_range(t);
+        if (dx * dx + dy * dy > r * r) return false;
+        int x = c % gd.W + dx, y = c / gd.W + dy;
+        if (x < 0 || y < 0 || x >= gd.W || y >= gd.H) return false;
+        uint32_t o = s_unit[y * gd.W + x];
+        int oo = u_owner(o);
+        return o != 0 && oo >= 0 && oo != owner;
+    }
+    }
+    return false;
+}
+
+// UnitAction.getValidActionArray for the idle unit at c: 79 bits (bit 0 = source)
+__device__ void cell_mask(const Grid& gd, int c, int player, const uint32_t* s_unit, const uint32_t* s_act,
+                          const uint8_t* s_wall, int res_player, uint32_t m[3]) {
+    m[0] = m[1] = m[2] = 0;
+    uint32_t u = s_unit[c];
+    if (u == 0 || u_owner(u) != player || s_act[c] != 0) return;
+    auto setb = [&](int b) { m[b >> 5] |= 1u << (b & 31); };
+    const int T = 1, MV = 7, HV = 11, RT = 15, PD = 19, PT = 23, AT = 30;
+    setb(0);
+    setb(T + A_NONE);
+    int t = u_type(u), x = c % gd.W, y = c / gd.W;
+    int nb[4];
+    bool freec[4];
+    for (int d = 0; d < 4; d++) {
+        nb[d] = nb_cell(gd, c, d);
+        freec[d] = nb[d] >= 0 && !s_wall[nb[d]] && s_unit[nb[d]] == 0;
+    }
+    const int cc = MRTS_ATTACK_GRID / 2;
+    if (ut_can_attack(t)) {
+        int r = ut_range(t);
+        for (int dy = -r; dy <= r; dy++)
+            for (int dx = -r; dx <= r; dx++) {
+                if (dx * dx + dy * dy > r * r) continue;
+                int xx = x + dx, yy = y + dy;
+                if (xx < 0 || yy < 0 || xx >= gd.W || yy >= gd.H) continue;
+                uint32_t o = s_unit[yy * gd.W + xx];
+                int oo = u_owner(o);
+                if (o != 0 && oo >= 0 && oo != player) {
+                    setb(T + A_ATTACK);
+                    setb(AT + (cc + dy) * MRTS_ATTACK_GRID + (cc + dx));
+                }
+            }
+    }
+    if (ut_can_harvest(t)) {
+        int ur = u_res(u);
+        for (int d = 0; d < 4; d++) {
+            if (nb[d] < 0 || s_unit[nb[d]] == 0) continue;
+            uint32_t o = s_unit[nb[d]];
+            if (ur == 0 && u_type(o) == RESOURCE) {
+                setb(T + A_HARVEST);
+                setb(HV + d);
+            }
+            if (ur > 0 && ut_is_stockpile(u_type(o)) && u_owner(o) == player) {
+                setb(T + A_RETURN);
+                setb(RT + d);
+            }
+        }
+    }
+    int prod = ut_produces(t);
+    bool anyfree = freec[0] || freec[1] || freec[2] || freec[3];
+    if (prod && anyfree) {
+        for (int ut = 0; ut < MRTS_NTYPES; ut++) {
+            if (!((prod >> ut) & 1) || res_player < ut_cost(ut)) continue;
+            setb(T + A_PRODUCE);
+            setb(PT + ut);
+            for (int d = 0; d < 4; d++)
+                if (freec[d]) setb(PD + d);
+        }
+    }
+    if (ut_can_move(t) && anyfree) {
+        setb(T + A_MOVE);
+        for (int d = 0; d < 4; d++)
+            if (freec[d]) setb(MV + d);
+    }
+}
+
+// one-hot word of vec_env.py:311-321 for the cell (perspective `player`)
+__device__ __forceinline__ uint32_t cell_onehot(uint32_t u, uint32_t a, uint8_t wall, int player) {
+    uint32_t b = 0;
+    if (u == 0) {
+        b = 1u | (1u << 5) | (1u << 10) | (1u << 13) | (1u << 21);
+    } else {
+        int hp = min(max(u_hp(u), 0), 4), res = min(u_res(u), 4), ow = u_owner(u);
+        int rel = ow < 0 ? 0 : (ow == player ? 1 : 2);
+        int at = a ? min(code_type(act_code(a)), 5) : 0;
+        b = (1u << hp) | (1u << (5 + res)) | (1u << (10 + rel)) | (1u << (13 + u_type(u) + 1)) | (1u << (21 + at));
+    }
+    return b | (1u << (27 + (wall ? 1 : 0)));
+}
+
+// ---------------------------------------------------------------------------
+// LDS carving (all dynamic, 16-byte aligned pieces: cdna_hip_programming §6 G17)
+struct Lds {
+    uint32_t* unit;
+    int32_t* uid;
+    uint32_t* act;
+    uint32_t* seq;
+    uint32_t* aux;   // decoded rows, then one-hot / mask bit words
+    int32_t* resv;   // reservation holder per cell
+    int32_t* list;   // compact cell lists
+    int32_t* prod;   // pending produce cells
+    int4* snap;      // ready-action snapshots
+    uint32_t* mbits; // mask bits, 3 words per cell (mask kernel)
+    uint8_t* wall;
+    unsigned long long* ballot;
+    uint32_t* posbits;
+    int* sc;         // scalars
+};
+enum { SC_TIME = 0, SC_RES0, SC_RES1, SC_UID, SC_STEPS, SC_MAP, SC_ERR, SC_NPROD, SC_CNT, SC_GO, SC_WIN,
+       SC_R0 = 16, /* rewards: [player][6] as ints */ SC_WORDS = 32 };
+
+__host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
+    size_t b = 0;
+    b += a16(4 * (size_t)HW) * 9;  // unit uid act seq aux resv list prod + spare
+    b += a16(16 * (size_t)HW);     // snap
+    b += a16(12 * (size_t)HW);     // mbits
+    b += a16((size_t)HW);          // wall
+    b += a16(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
+    b += a16(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
+    b += a16(4 * SC_WORDS);
+    return b;
+}
+
+__device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
+    Lds L;
+    size_t o = 0;
+    auto take = [&](size_t n) { unsigned char* p = base + o; o += a16(n); return p; };
+    L.unit = (uint32_t*)take(4 * (size_t)HW);
+    L.uid = (int32_t*)take(4 * (size_t)HW);
+    L.act = (uint32_t*)take(4 * (size_t)HW);
+    L.seq = (uint32_t*)take(4 * (size_t)HW);
+    L.aux = (uint32_t*)take(4 * (size_t)HW);
+    L.resv = (int32_t*)take(4 * (size_t)HW);
+    L.list = (int32_t*)take(4 * (size_t)HW);
+    L.prod = (int32_t*)take(4 * (size_t)HW);
+    take(4 * (size_t)HW);
+    L.snap = (int4*)take(16 * (size_t)HW);
+    L.mbits = (uint32_t*)take(12 * (size_t)HW);
+    L.wall = (uint8_t*)take((size_t)HW);
+    L.ballot = (unsigned long long*)take(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
+    L.posbits = (uint32_t*)take(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
+    L.sc = (int*)take(4 * SC_WORDS);
+    return L;
+}
+
+// Ordered block-wide compaction: list <- cells c (ascending) with pred(c).
+template <int NT, typename F>
+__device__ int compact_cells(int HW, F pred, int32_t* list, unsigned long long* s_mask) {
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int J = (HW + NT - 1) / NT;
+    for (int j = 0; j < J; j++) {
+        int c = j * NT + threadIdx.x;
+        bool f = c < HW && pred(c);
+        unsigned long long m = __ballot(f);
+        if (lane == 0) s_mask[j * NW + w] = m;
+    }
+    __syncthreads();
+    int total = 0;
+    for (int j = 0; j < J; j++) {
+        int mi = j * NW + w;
+        int before = 0;
+        for (int k = 0; k < J * NW; k++) {
+            int pc = __popcll(s_mask[k]);
+            if (k < mi) before += pc;
+            if (j == 0) total += pc;
+        }
+        unsigned long long m = s_mask[mi];
+        if ((m >> lane) & 1ull) list[before + __popcll(m & ((1ull << lane) - 1ull))] = j * NT + threadIdx.x;
+    }
+    __syncthreads();
+    return total;
+}
+
+struct Game {
+    int g, env0, nviews, selfplay;
+};
+__device__ __forceinline__ Game game_of(const EngineParams& p, int g) {
+    Game G;
+    G.g = g;
+    G.selfplay = g < p.nsp_games;
+    G.env0 = G.selfplay ? 2 * g : p.nsp + (g - p.nsp_games);
+    G.nviews = G.selfplay ? 2 : 1;
+    return G;
+}
+
+// PhysicalGameState.load + new GameState into LDS
+template <int NT>
+__device__ void reset_into_lds(const EngineParams& p, const Lds& L, int map) {
+    const int HW = p.HW;
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        int4 v = p.map_cells[(size_t)map * HW + c];
+        L.unit[c] = (uint32_t)v.x;
+        L.uid[c] = v.y;
+        L.act[c] = 0;
+        L.seq[c] = 0;
+        L.wall[c] = p.map_wall[(size_t)map * HW + c];
+    }
+    if (threadIdx.x == 0) {
+        const int* ms = p.map_scal + (size_t)map * MRTS_MAP_SCALARS;
+        L.sc[SC_TIME] = 0;
+        L.sc[SC_RES0] = ms[MRTS_M_RES0];
+        L.sc[SC_RES1] = ms[MRTS_M_RES1];
+        L.sc[SC_UID] = ms[MRTS_M_NUNITS];
+        L.sc[SC_STEPS] = 0;
+        L.sc[SC_MAP] = map;
+    }
+}
+
+template <int NT>
+__device__ void load_game(const EngineParams& p, const Lds& L, int g) {
+    if (threadIdx.x < MRTS_GENV_WORDS) L.sc[threadIdx.x] = p.genv[(size_t)g * MRTS_GENV_WORDS + threadIdx.x];
+    __syncthreads();
+    const int HW = p.HW, map = L.sc[SC_MAP];
+    const int4* src = p.cells + (size_t)g * HW;
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        int4 v = src[c];
+        L.unit[c] = (uint32_t)v.x;
+        L.uid[c] = v.y;
+        L.act[c] = (uint32_t)v.z;
+        L.seq[c] = (uint32_t)v.w;
+        L.wall[c] = p.map_wall[(size_t)map * HW + c];
+    }
+    __syncthreads();
+}
+
+template <int NT>
+__device__ void store_game(const EngineParams& p, const Lds& L, int g) {
+    const int HW = p.HW;
+    int4* dst = p.cells + (size_t)g * HW;
+    for (int c = threadIdx.x; c < HW; c += NT) dst[c] = make_int4((int)L.unit[c], L.uid[c], (int)L.act[c], (int)L.seq[c]);
+    if (threadIdx.x < MRTS_GENV_WORDS) p.genv[(size_t)g * MRTS_GENV_WORDS + threadIdx.x] = L.sc[threadIdx.x];
+}
+
+// write the one-hot observation of one view: bits in L.aux, 16-byte stores
+template <int NT, int P, typename OT>
+__device__ void write_obs(const EngineParams& p, const Lds& L, int env, int player) {
+    const int HW = p.HW;
+    for (int c = threadIdx.x; c < HW; c += NT) L.aux[c] = cell_onehot(L.unit[c], L.act[c], L.wall[c], player);
+    __syncthreads();
+    OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)env * HW * P;
+    const int total = HW * P;
+    if ((total & 3) == 0) {
+        using V4 = typename std::conditional<std::is_same<OT, float>::value, float4, int4>::type;
+        V4* o4 = reinterpret_cast<V4*>(out);
+        for (int k = threadIdx.x; k < total / 4; k += NT) {
+            int e = 4 * k;
+            int c = e / P, pl = e - c * P;
+            OT v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[j] = (OT)((L.aux[c] >> pl) & 1u);
+                if (++pl == P) { pl = 0; c++; }
+            }
+            V4 w;
+            w.x = v[0]; w.y = v[1]; w.z = v[2]; w.w = v[3];
+            o4[k] = w;
+        }
+    } else {
+        for (int e = threadIdx.x; e < total; e += NT) out[e] = (OT)((L.aux[e / P] >> (e % P)) & 1u);
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Reset kernel: every game (or the listed ones) back to its map; obs out.
+template <int NT, int P, typename OT>
+__global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* games, const int32_t* maps, int count) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Lds L = carve(smem, p.HW, p.W, NT);
+    int g = games ? games[blockIdx.x] : blockIdx.x;
+    int map = maps ? maps[blockIdx.x] : p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
+    if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
+    __syncthreads();
+    reset_into_lds<NT>(p, L, map);
+    __syncthreads();
+    store_game<NT>(p, L, g);
+    Game G = game_of(p, g);
+    for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
+}
+
+// ---------------------------------------------------------------------------
+// Mask kernel: JNIGridnetVecClient.getMasks(0) -> [N][HW][78] + source [N][HW]
+template <int NT>
+__global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Lds L = carve(smem, p.HW, p.W, NT);
+    const int g = blockIdx.x, HW = p.HW;
+    load_game<NT>(p, L, g);
+    Grid gd{p.W, p.H, HW};
+    Game G = game_of(p, g);
+    for (int v = 0; v < G.nviews; v++) {
+        const int env = G.env0 + v, player = v;
+        const int res = player == 0 ? L.sc[SC_RES0] : L.sc[SC_RES1];
+        for (int c = threadIdx.x; c < HW; c += NT) {
+            uint32_t m[3];
+            cell_mask(gd, c, player, L.unit, L.act, L.wall, res, m);
+            L.mbits[3 * c] = m[0];
+            L.mbits[3 * c + 1] = m[1];
+            L.mbits[3 * c + 2] = m[2];
+            p.src_out[(size_t)env * HW + c] = (int32_t)(m[0] & 1u);
+        }
+        __syncthreads();
+        int32_t* out = p.mask + (size_t)env * HW * MRTS_MASK_CH;
+        const int total = HW * MRTS_MASK_CH;
+        if ((total & 3) == 0) {
+            int4* o4 = reinterpret_cast<int4*>(out);
+            for (int k = threadIdx.x; k < total / 4; k += NT) {
+                int e = 4 * k;
+                int c = e / MRTS_MASK_CH, ch = e - c * MRTS_MASK_CH;
+                int v4[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    int b = ch + 1;
+                    v4[j] = (int)((L.mbits[3 * c + (b >> 5)] >> (b & 31)) & 1u);
+                    if (++ch == MRTS_MASK_CH) { ch = 0; c++; }
+                }
+                o4[k] = make_int4(v4[0], v4[1], v4[2], v4[3]);
+            }
+        } else {
+            for (int e = threadIdx.x; e < total; e += NT) {
+                int c = e / MRTS_MASK_CH, b = e % MRTS_MASK_CH + 1;
+                out[e] = (int)((L.mbits[3 * c + (b >> 5)] >> (b & 31)) & 1u);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Step kernel: JNIGridnetVecClient.gameStep for one game per workgroup.
+enum : uint32_t { CAND = 1u << 31, LEGAL = 1u << 30 };
+
+__device__ __forceinline__ int res_of(const Lds& L, int player) { return L.sc[SC_RES0 + player]; }
+
+// PlayerAction.fromVectorAction consistency filter + GameState.issueSafe/issue
+// for one player's rows (lane 0 only).  Rows are L.list[0..n) ascending.
+__device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd, int q, int n) {
+    const int time = L.sc[SC_TIME];
+    // --- fromVectorAction: ResourceUsage.consistentWith(pa.ru) ----------------
+    const int nposw = (gd.HW + 2 * gd.W + 31) / 32;
+    for (int i = 0; i < nposw; i++) L.posbits[i] = 0;
+    int pa_cost = 0;
+    for (int i = 0; i < n; i++) {
+        int c = L.list[i];
+        uint32_t nw = L.aux[c];
+        if (u_owner(L.unit[c]) != q) continue;
+        int code = (int)(nw & 0xFFFu), type = code_type(code);
+        if (type != A_MOVE && type != A_PRODUCE) continue;
+        const int off[4] = {-gd.W, 1, gd.W, -1};
+        int pos = c + off[code_param(code)];   // unchecked, as x + y*W + offset
+        int cost = type == A_PRODUCE ? ut_cost(code_utype(code)) : 0;
+        int bi = pos + gd.W;
+        bool taken = (L.posbits[bi >> 5] >> (bi & 31)) & 1u;
+        int s = cost + pa_cost;
+        if (taken || (s > 0 && s > res_of(L, q))) {
+            L.aux[c] = nw & ~CAND;   // dropped: gets fillWithNones
+            continue;
+        }
+        L.posbits[bi >> 5] |= 1u << (bi & 31);
+        pa_cost += cost;
+    }
+    // --- issueSafe + issue -----------------------------------------------------
+    int* rw = L.sc + SC_R0 + 6 * q;
+    for (int i = 0; i < n; i++) {
+        int c = L.list[i];
+        uint32_t nw = L.aux[c];
+        if (u_owner(L.unit[c]) != q || !(nw & CAND)) continue;
+        const int ut = u_type(L.unit[c]);
+        int code = (int)(nw & 0xFFFu);
+        // issueSafe: illegal -> NONE with the same ETA
+        int cur = code, cur_dur = 1;   // cur_dur: duration when cur is NONE
+        if (code_type(code) == A_NONE) cur_dur = 1;
+        else if (!(nw & LEGAL)) { cur_dur = eta_code(code, ut); cur = A_NONE; }
+        int te = cur;                  // the action the TraceEntry records
+        const int ctype = code_type(cur);
+        int pos = -1, cost_new = 0;
+        if (ctype == A_MOVE || ctype == A_PRODUCE) pos = nb_cell(gd, c, code_param(cur));
+        if (ctype == A_PRODUCE) cost_new = ut_cost(code_utype(cur));
+        // uaa's inconsistent with the new ResourceUsage, in LinkedHashMap order
+        int cand[16];
+        int nc = 0;
+        if (pos >= 0 && L.resv[pos] >= 0) cand[nc++] = L.resv[pos];
+        const int nprod = L.sc[SC_NPROD];
+        for (int k = 0; k < nprod; k++) {
+            int pc = L.prod[k];
+            uint32_t pa = L.act[pc];
+            if (pa == 0 || code_type(act_code(pa)) != A_PRODUCE) continue;
+            int pp = u_owner(L.unit[pc]), cp = ut_cost(code_utype(act_code(pa)));
+            bool bad = false;
+            for (int pl = 0; pl < 2; pl++) {
+                int s = (pp == pl ? cp : 0) + (q == pl ? cost_new : 0);
+                if (s > 0 && s > res_of(L, pl)) bad = true;
+            }
+            if (!bad) continue;
+            bool dup = false;
+            for (int j = 0; j < nc; j++) dup |= cand[j] == pc;
+            if (!dup && nc < 16) cand[nc++] = pc;
+        }
+        for (int a = 1; a < nc; a++) {   // insertion sort by issue sequence
+            int x = cand[a];
+            int b = a - 1;
+            while (b >= 0 && L.seq[cand[b]] > L.seq[x]) { cand[b + 1] = cand[b]; b--; }
+            cand[b + 1] = x;
+        }
+        bool original = true;
+        for (int k = 0; k < nc; k++) {
+            int cc = cand[k];
+            uint32_t ua = L.act[cc];
+            if (seq_time(L.seq[cc]) == time) {    // CANCEL_BOTH
+                int ucode = act_code(ua);
+                int d1 = eta_code(ucode, u_type(L.unit[cc]));
+                int d2 = code_type(cur) == A_NONE ? cur_dur : eta_code(cur, ut);
+                int d = min(d1, d2);
+                int utp = code_type(ucode);
+                if (utp == A_MOVE || utp == A_PRODUCE) {
+                    int rp = nb_cell(gd, cc, code_param(ucode));
+                    if (rp >= 0 && L.resv[rp] == cc) L.resv[rp] = -1;
+                }
+                L.act[cc] = act_make(A_NONE, time + d);
+                cur = A_NONE;
+                cur_dur = d;
+                original = false;
+            } else {                               // "Inconsistent actions were executed!"
+                cur = A_NONE;
+                cur_dur = -1;
+                if (original) te = A_NONE;
+            }
+        }
+        const int ft = code_type(cur);
+        const int done = ft == A_NONE ? time + cur_dur : time + eta_code(cur, ut);
+        L.act[c] = act_make(cur, done);
+        L.seq[c] = seq_make(time, q, c);
+        if (ft == A_MOVE || ft == A_PRODUCE) {
+            L.resv[nb_cell(gd, c, code_param(cur))] = c;
+            if (ft == A_PRODUCE) L.prod[L.sc[SC_NPROD]++] = c;
+        }
+        // ai.reward.* on the TraceEntry actions
+        const int tt = code_type(te);
+        if (tt == A_HARVEST || tt == A_RETURN) rw[1]++;
+        if (tt == A_PRODUCE) {
+            int pu = code_utype(te);
+            if (pu == WORKER) rw[2]++;
+            else if (pu == BASE || pu == BARRACKS) rw[3]++;
+            else if (pu >= LIGHT) rw[5]++;
+        }
+        if (tt == A_ATTACK) rw[4]++;
+    }
+}
+
+// UnitAction.execute for one ready assignment (lane 0), from its snapshot
+__device__ void execute_one(const Lds& L, const Grid& gd, int4 s) {
+    const int c = s.x;
+    const uint32_t u = (uint32_t)s.y;
+    const int code = (int)(s.z);
+    const int uid = s.w;
+    const int t = u_type(u), owner = u_owner(u);
+    const bool here = L.unit[c] != 0 && L.uid[c] == uid;   // not killed earlier this cycle
+    const int type = code_type(code), param = code_param(code);
+    switch (type) {
+    case A_MOVE: {
+        if (!here) break;
+        int n = nb_cell(gd, c, param);
+        if (n < 0 || L.unit[n] != 0) { L.sc[SC_ERR] |= MRTS_ERR_MOVE_OCCUPIED; break; }
+        L.unit[n] = L.unit[c];
+        L.uid[n] = uid;
+        L.act[n] = 0;
+        L.seq[n] = 0;
+        L.unit[c] = 0;
+        L.uid[c] = 0;
+        L.act[c] = 0;
+        L.seq[c] = 0;
+        break;
+    }
+    case A_ATTACK: {
+        int dx = param % MRTS_ATTACK_GRID - MRTS_ATTACK_GRID / 2, dy = param / MRTS_ATTACK_GRID - MRTS_ATTACK_GRID / 2;
+        int x = c % gd.W + dx, y = c / gd.W + dy;
+        if (x < 0 || y < 0 || x >= gd.W || y >= gd.H) break;
+        int n = y * gd.W + x;
+        uint32_t o = L.unit[n];
+        if (o == 0) break;
+        int hp = u_hp(o) - ut_damage(t);   // VERSION_ORIGINAL: min == max damage
+        if (hp <= 0) {                     // GameState.removeUnit (+ its assignment)
+            L.unit[n] = 0;
+            L.uid[n] = 0;
+            L.act[n] = 0;
+            L.seq[n] = 0;
+        } else {
+            L.unit[n] = u_with_hp(o, hp);
+        }
+        break;
+    }
+    case A_HARVEST: {
+        int n = nb_cell(gd, c, param);
+        if (n < 0) break;
+        uint32_t o = L.unit[n];
+        if (o == 0 || u_type(o) != RESOURCE || !ut_can_harvest(t) || u_res(u) != 0) break;
+        int left = u_res(o) - ut_harvest_amount(t);
+        if (left <= 0) {
+            L.unit[n] = 0;
+            L.uid[n] = 0;
+            L.act[n] = 0;
+            L.seq[n] = 0;
+        } else {
+            L.unit[n] = u_with_res(o, left);
+        }
+        if (here) L.unit[c] = u_with_res(L.unit[c], ut_harvest_amount(t));
+        break;
+    }
+    case A_RETURN: {
+        int n = nb_cell(gd, c, param);
+        if (n < 0) break;
+        uint32_t o = L.unit[n];
+        if (o == 0 || !ut_is_stockpile(u_type(o)) || u_res(u) <= 0) break;
+        L.sc[SC_RES0 + owner] += u_res(u);
+        if (here) L.unit[c] = u_with_res(L.unit[c], 0);
+        break;
+    }
+    case A_PRODUCE: {
+        int n = nb_cell(gd, c, param);
+        int put = code_utype(code);
+        if (n < 0 || L.unit[n] != 0) { L.sc[SC_ERR] |= MRTS_ERR_PRODUCE_OCCUPIED; break; }
+        L.unit[n] = u_make(put, owner, ut_hp(put), 0);
+        L.uid[n] = L.sc[SC_UID]++;
+        L.act[n] = 0;
+        L.seq[n] = 0;
+        L.sc[SC_RES0 + owner] -= ut_cost(put);
+        break;
+    }
+    default: break;
+    }
+}
+
+template <int NT, int P, typename OT>
+__global__ __launch_bounds__(NT) void k_step(EngineParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int HW = p.HW;
+    Lds L = carve(smem, HW, p.W, NT);
+    const int g = blockIdx.x;
+    const Grid gd{p.W, p.H, HW};
+    const Game G = game_of(p, g);
+    if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
+    __syncthreads();
+    load_game<NT>(p, L, g);
+    const int time = L.sc[SC_TIME];
+
+    // (1) decode the rows of every idle unit whose cell is in source_unit_mask
+    //     (vec_env.py:972-974) + Unit.canExecuteAction, lane-parallel.
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        uint32_t u = L.unit[c], nw = 0;
+        int ow = u_owner(u);
+        L.resv[c] = -1;
+        if (u != 0 && ow >= 0 && L.act[c] == 0) {
+            int view = G.selfplay ? ow : (ow == 0 ? 0 : -1);
+            if (view >= 0) {
+                const size_t row = (size_t)(G.env0 + view) * HW + c;
+                if (p.src[row]) {
+                    const int64_t* r = p.actions + row * 7;
+                    int64_t ty = r[0];
+                    int code = -1;
+                    if (ty == A_NONE) code = code_make(A_NONE, 0, 0);
+                    else if (ty >= A_MOVE && ty <= A_RETURN) {
+                        int64_t d = r[ty];
+                        if (d >= 0 && d < 4) code = code_make((int)ty, (int)d, 0);
+                    } else if (ty == A_PRODUCE) {
+                        int64_t d = r[4], t2 = r[5];
+                        if (d >= 0 && d < 4 && t2 >= 0 && t2 < MRTS_NTYPES) code = code_make(A_PRODUCE, (int)d, (int)t2);
+                    } else if (ty == A_ATTACK) {
+                        int64_t a = r[6];
+                        if (a >= 0 && a < MRTS_ATTACK_GRID * MRTS_ATTACK_GRID) code = code_make(A_ATTACK, (int)a, 0);
+                    }
+                    if (code >= 0) {
+                        bool lg = legal_code(gd, c, code, L.unit, L.wall, res_of(L, ow));
+                        nw = CAND | (lg ? LEGAL : 0u) | (uint32_t)code;
+                    }
+                }
+            }
+        }
+        L.aux[c] = nw;
+    }
+    __syncthreads();
+    // pending move/produce reservations (ResourceUsage of unitActions)
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        uint32_t a = L.act[c];
+        if (a) {
+            int code = act_code(a), ty = code_type(code);
+            if (ty == A_MOVE || ty == A_PRODUCE) {
+                int n = nb_cell(gd, c, code_param(code));
+                if (n >= 0) L.resv[n] = c;
+            }
+        }
+    }
+    int nprod = compact_cells<NT>(HW, [&](int c) {
+        uint32_t a = L.act[c];
+        return a != 0 && code_type(act_code(a)) == A_PRODUCE;
+    }, L.prod, L.ballot);
+    int nrows = compact_cells<NT>(HW, [&](int c) { return (L.aux[c] & CAND) != 0; }, L.list, L.ballot);
+    // (2) ordered part: p0 then p1 (bot envs: the passive bot issues only NONEs)
+    if (threadIdx.x == 0) {
+        L.sc[SC_NPROD] = nprod;
+        issue_player(p, L, gd, 0, nrows);
+        if (G.selfplay) issue_player(p, L, gd, 1, nrows);
+    }
+    __syncthreads();
+    // (3) fillWithNones(gs, player, 1) for every idle unit (both players)
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        uint32_t u = L.unit[c];
+        if (u != 0 && u_owner(u) >= 0 && L.act[c] == 0) {
+            L.act[c] = act_make(A_NONE, time + 1);
+            L.seq[c] = seq_make(time, u_owner(u), 4095);
+        }
+    }
+    __syncthreads();
+    // (4) GameState.cycle(): time++, execute ready assignments in issue order
+    const int now = time + 1;
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        uint32_t a = L.act[c];
+        if (a && act_done(a) <= now && code_type(act_code(a)) == A_NONE) L.act[c] = 0;
+    }
+    int nready = compact_cells<NT>(HW, [&](int c) {
+        uint32_t a = L.act[c];
+        return a != 0 && act_done(a) <= now;
+    }, L.list, L.ballot);
+    if (threadIdx.x == 0) {
+        L.sc[SC_TIME] = now;
+        if (now >= MRTS_MAX_TIME) L.sc[SC_ERR] |= MRTS_ERR_TIME_OVERFLOW;
+        if (nready > 0) {
+            for (int i = 0; i < nready; i++) {
+                int c = L.list[i];
+                L.snap[i] = make_int4(c, (int)L.unit[c], act_code(L.act[c]), L.uid[c]);
+                L.resv[i] = (int)L.seq[c];
+            }
+            for (int i = 0; i < nready; i++) L.act[L.list[i]] = 0;   // unitActions.remove
+            for (int a = 1; a < nready; a++) {                      // LinkedHashMap order
+                int4 x = L.snap[a];
+                int xs = L.resv[a];
+                int b = a - 1;
+                while (b >= 0 && (uint32_t)L.resv[b] > (uint32_t)xs) {
+                    L.snap[b + 1] = L.snap[b];
+                    L.resv[b + 1] = L.resv[b];
+                    b--;
+                }
+                L.snap[b + 1] = x;
+                L.resv[b + 1] = xs;
+            }
+            for (int i = 0; i < nready; i++) execute_one(L, gd, L.snap[i]);
+        }
+    }
+    __syncthreads();
+    // (5) PhysicalGameState.gameover / winner
+    int has0 = 0, has1 = 0;
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        int ow = u_owner(L.unit[c]);
+        has0 |= (L.unit[c] != 0 && ow == 0);
+        has1 |= (L.unit[c] != 0 && ow == 1);
+    }
+    has0 = __syncthreads_or(has0);
+    has1 = __syncthreads_or(has1);
+    const bool gameover = !(has0 && has1);
+    const int winner = (has0 && !has1) ? 0 : (has1 && !has0) ? 1 : -1;
+    // (6) rewards / done (JNIGridnetVecClient.gameStep terminal handling)
+    const int steps = L.sc[SC_STEPS] + 1;
+    const bool reset = gameover || steps >= p.max_steps;
+    if (threadIdx.x < 6 * G.nviews) {
+        int v = threadIdx.x / 6, k = threadIdx.x % 6;
+        int env = G.env0 + v;
+        double r = k == 0 ? (gameover ? (winner == v ? 1.0 : -1.0) : 0.0) : (double)L.sc[SC_R0 + 6 * v + k];
+        p.raw_reward[(size_t)env * 6 + k] = r;
+        p.done[(size_t)env * 6 + k] = (uint8_t)((gameover || (k == 0 && reset)) ? 1 : 0);
+    }
+    __syncthreads();
+    if (reset) {
+        reset_into_lds<NT>(p, L, L.sc[SC_MAP]);
+        __syncthreads();
+    } else if (threadIdx.x == 0) {
+        L.sc[SC_STEPS] = steps;
+    }
+    __syncthreads();
+    // (7) write back + one-hot observation of every view
+    store_game<NT>(p, L, g);
+    for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based masked sampler (hello_world.py:27-64 semantics), Philox4x32-10
+// keyed (seed) with counter (cell, env, step, half) -- identical stream to the
+// oracle's ovec_sample_actions.  One lane per (env, cell).
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed, uint32_t step,
+                                                int64_t* __restrict__ act) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n * hw) return;
+    const int e = idx / hw, c = idx - e * hw;
+    // 78 int32 = 39 x 8-byte loads (rows are 312 B, 8-byte aligned)
+    const int2* m2 = reinterpret_cast<const int2*>(mask + (size_t)idx * MRTS_MASK_CH);
+    uint32_t bits[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < MRTS_MASK_CH / 2; j++) {
+        int2 v = m2[j];
+        int b = 2 * j;
+        if (v.x) bits[b >> 5] |= 1u << (b & 31);
+        if (v.y) bits[(b + 1) >> 5] |= 1u << ((b + 1) & 31);
+    }
+    uint32_t r[8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
+        philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        r[4 * h] = ctr[0]; r[4 * h + 1] = ctr[1]; r[4 * h + 2] = ctr[2]; r[4 * h + 3] = ctr[3];
+    }
+    const int off[7] = {0, 6, 10, 14, 18, 22, 29};
+    const int len[7] = {6, 4, 4, 4, 4, 7, 49};
+    int64_t out[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        int nvalid = 0;
+        for (int j = 0; j < len[k]; j++) nvalid += (bits[(off[k] + j) >> 5] >> ((off[k] + j) & 31)) & 1u;
+        int pick = 0;
+        if (nvalid == 0) {
+            pick = (int)(((uint64_t)r[k] * (uint32_t)len[k]) >> 32);
+        } else {
+            int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
+            for (int j = 0; j < len[k]; j++) {
+                if ((bits[(off[k] + j) >> 5] >> ((off[k] + j) & 31)) & 1u) {
+                    if (t == 0) { pick = j; break; }
+                    t--;
+                }
+            }
+        }
+        out[k] = pick;
+    }
+    int64_t* o = act + (size_t)idx * 7;
+#pragma unroll
+    for (int k = 0; k < 7; k++) o[k] = out[k];
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+template <int NT>
+static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
+    size_t sh = lds_bytes(p.HW, p.W, NT);
+    int grid = p.G;
+    if (kind == 0) {   // reset
+        grid = games ? count : p.G;
+        if (grid == 0) return hipSuccess;
+        if (p.obs_float) hipLaunchKernelGGL((k_reset<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+        else hipLaunchKernelGGL((k_reset<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+    } else if (kind == 1) {
+        hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
+    } else {
+        if (p.obs_float) hipLaunchKernelGGL((k_step<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p);
+        else hipLaunchKernelGGL((k_step<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+    }
+    return hipGetLastError();
+}
+
+static hipError_t dispatch(const EngineParams& p, int kind, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
+    if (p.HW <= 64) return launch_all<64>(p, kind, s, games, maps, count);
+    if (p.HW <= 128) return launch_all<128>(p, kind, s, games, maps, count);
+    return launch_all<256>(p, kind, s, games, maps, count);
+}
+
+}  // namespace mrts
+
+extern "C" {
+hipError_t mrts_engine_reset(const EngineParams* p, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
+    return mrts::dispatch(*p, 0, s, games, maps, count);
+}
+hipError_t mrts_engine_masks(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 1, s, nullptr, nullptr, 0); }
+hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 2, s, nullptr, nullptr, 0); }
+hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
+    int total = n * hw;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(mrts::k_sample, dim3((total + 255) / 256), dim3(256), 0, s, mask, n, hw, seed, step, act);
+    return hipGetLastError();
+}
+size_t mrts_engine_lds_bytes(int HW, int W) {
+    int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
+    return mrts::lds_bytes(HW, W, NT);
+}
+}

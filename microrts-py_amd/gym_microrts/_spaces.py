@@ -1,0 +1,53 @@
+"""Observation / action spaces of MicroRTSGridModeVecEnv.
+
+Uses gym.spaces when gym is importable (the reference constructs
+gym.spaces.Box / MultiDiscrete at vec_env.py:242-252).  gym is not installed in
+this image, so a minimal stand-in with the attributes the drivers read
+(`shape`, `dtype`, `nvec`, `seed`, `sample`, `contains`) is provided.
+"""
+import numpy as np
+
+try:  # pragma: no cover - depends on the environment
+    from gym.spaces import Box, MultiDiscrete  # noqa: F401
+except Exception:  # gym absent
+
+    class _Space:
+        def __init__(self, shape, dtype):
+            self.shape = tuple(shape)
+            self.dtype = np.dtype(dtype)
+            self.np_random = np.random.default_rng()
+
+        def seed(self, seed=None):
+            self.np_random = np.random.default_rng(seed)
+            return [seed]
+
+    class Box(_Space):
+        def __init__(self, low, high, shape, dtype=np.float32):
+            super().__init__(shape, dtype)
+            self.low = np.full(self.shape, low, dtype=self.dtype)
+            self.high = np.full(self.shape, high, dtype=self.dtype)
+
+        def sample(self):
+            return self.np_random.integers(self.low, self.high + 1, size=self.shape).astype(self.dtype)
+
+        def contains(self, x):
+            x = np.asarray(x)
+            return x.shape == self.shape and bool(np.all(x >= self.low)) and bool(np.all(x <= self.high))
+
+        def __repr__(self):
+            return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+    class MultiDiscrete(_Space):
+        def __init__(self, nvec, dtype=np.int64):
+            self.nvec = np.asarray(nvec, dtype=np.int64)
+            super().__init__(self.nvec.shape, dtype)
+
+        def sample(self):
+            return (self.np_random.random(self.nvec.shape) * self.nvec).astype(self.dtype)
+
+        def contains(self, x):
+            x = np.asarray(x)
+            return x.shape == self.shape and bool(np.all(x >= 0)) and bool(np.all(x < self.nvec))
+
+        def __repr__(self):
+            return f"MultiDiscrete({self.nvec})"

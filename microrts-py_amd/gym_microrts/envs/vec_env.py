@@ -1,0 +1,371 @@
+"""MicroRTSGridModeVecEnv on the MI355X engine.
+
+Keeps the constructor signature and the reset / get_action_mask / step surface of
+/root/reference/gym_microrts/envs/vec_env.py:38-1101 so that
+experiments/ppo_gridnet.py runs unmodified.  Everything the reference does in
+Java (JNIGridnetVecClient over JPype) and in the per-env numpy loops
+(_encode_obs, action packing, reward weighting) happens in libmicrorts_amd.so
+kernels on the GPU; this class only moves buffers and keeps the Python contract.
+
+Return types
+  * default (return_tensors=False): exactly the reference's -- numpy int32 obs
+    (N,H,W,29), numpy int32 masks (N,H*W,78), numpy float64 rewards, numpy bool
+    dones, a list of {"raw_rewards": row} dicts.
+  * return_tensors=True: device-resident torch tensors (obs float32 by default,
+    masks int32, rewards float64, dones bool) and a lazily materialised infos
+    sequence.  Tensors alias engine-owned buffers that are overwritten by the
+    next call (the ownership rule of the reference's shared-memory env,
+    vec_env.py:1331-1362).
+"""
+import json
+import os
+import xml.etree.ElementTree as ET
+from enum import Enum
+from itertools import cycle
+
+import numpy as np
+import torch
+
+import gym_microrts
+from gym_microrts import _native
+from gym_microrts._native import MicroRTSError, MicroRTSNotImplemented
+from gym_microrts._spaces import Box, MultiDiscrete
+
+RF_NAMES = [
+    "WinLossRewardFunction",
+    "ResourceGatherRewardFunction",
+    "ProduceWorkerRewardFunction",
+    "ProduceBuildingRewardFunction",
+    "AttackRewardFunction",
+    "ProduceCombatUnitRewardFunction",
+]
+
+
+class RewardFunction:
+    """Stand-in for the ai.reward.* Java objects of vec_env.py:185-195; callers
+    only use str(rf) (ppo_gridnet.py:145-147, league.py:278)."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __str__(self):
+        return self.name
+
+    __repr__ = __str__
+
+
+class LazyInfos:
+    """list[dict] view over the (N,6) raw-reward tensor, materialised on access
+    (the per-env dict creation of vec_env.py:1036 is the host cost avoided)."""
+
+    def __init__(self, raw):
+        self._raw = raw
+        self._np = None
+
+    def _rows(self):
+        if self._np is None:
+            self._np = self._raw.detach().cpu().numpy()
+        return self._np
+
+    def __len__(self):
+        return self._raw.shape[0]
+
+    def __getitem__(self, i):
+        rows = self._rows()
+        if isinstance(i, slice):
+            return [{"raw_rewards": r} for r in rows[i]]
+        return {"raw_rewards": rows[i]}
+
+    def __iter__(self):
+        for r in self._rows():
+            yield {"raw_rewards": r}
+
+
+class MicroRTSGridModeVecEnv:
+    metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 150}
+
+    class PriorMode(Enum):
+        """vec_env.py:48-84.  Only NONE is supported (the KG prior is out of
+        scope)."""
+
+        NONE = "none"
+        APPEND_ENCODED = "append_encoded"
+        APPEND_RAW = "append_raw"
+        REWARD_ADVICE = "reward_advice"
+        REWARD_SHAPING = "reward_shaping"
+
+        def __bool__(self):
+            return self != self.NONE
+
+    def __init__(
+        self,
+        num_selfplay_envs,
+        num_bot_envs,
+        partial_obs=False,
+        max_steps=2000,
+        render_theme=2,
+        frame_skip=0,
+        ai2s=[],
+        map_paths=["maps/10x10/basesTwoWorkers10x10.xml"],
+        reward_shaping=True,
+        reward_weight=np.array([0.0, 1.0, 0.0, 0.0, 0.0, 5.0]),
+        cycle_maps=[],
+        autobuild=False,
+        jvm_args=[],
+        prior_mode="none",
+        reward_prior_weight=0.01,
+        prior_advice_freq=1,
+        seed=1,
+        runs_dir=".",
+        graph_ttl_file="graph.ttl",
+        graph_triples_file="triples.tsv",
+        *,
+        device=None,
+        return_tensors=False,
+        obs_dtype=None,
+    ):
+        # vec_env.py:110-127
+        self.num_selfplay_envs = num_selfplay_envs
+        self.num_bot_envs = num_bot_envs
+        self.num_envs = num_selfplay_envs + num_bot_envs
+        assert self.num_bot_envs == len(ai2s), "for each environment, a microrts ai should be provided"
+        self.partial_obs = partial_obs
+        self.max_steps = max_steps
+        self.render_theme = render_theme  # stored, unused (as in the reference)
+        self.frame_skip = frame_skip      # stored, unused (vec_env.py:116-117)
+        self.ai2s = ai2s
+        self.map_paths = map_paths
+        if len(map_paths) == 1:
+            self.map_paths = [map_paths[0] for _ in range(self.num_envs)]
+        else:
+            assert len(map_paths) == self.num_envs, "if multiple maps are provided, they should be provided for each environment"
+        self.reward_shaping = reward_shaping
+        self.reward_weight = reward_weight
+        self.prior_mode = self.PriorMode(prior_mode)
+        if self.prior_mode:
+            raise MicroRTSNotImplemented("prior_mode other than 'none' (KG prior) is out of scope")
+        self.microrts_path = os.path.join(gym_microrts.__path__[0], "microrts")
+        self.cycle_maps = list(map(lambda i: os.path.join(self.microrts_path, i), cycle_maps))
+        self.next_map = cycle(self.cycle_maps)
+
+        # read map (vec_env.py:148-150)
+        first = os.path.join(self.microrts_path, self.map_paths[0])
+        root = ET.parse(first).getroot()
+        self.height, self.width = int(root.get("height")), int(root.get("width"))
+
+        # map table: one entry per distinct path; envs of a selfplay pair share game 2k's map
+        full = [os.path.join(self.microrts_path, p) for p in self.map_paths]
+        self._map_table = []
+        for p in full + self.cycle_maps:
+            if p not in self._map_table:
+                self._map_table.append(p)
+        self._map_index = {p: i for i, p in enumerate(self._map_table)}
+        nsp_games = num_selfplay_envs // 2
+        game_env = [2 * k for k in range(nsp_games)] + [num_selfplay_envs + j for j in range(num_bot_envs)]
+        game_map = [self._map_index[full[e]] for e in game_env]
+
+        # opponents (vec_env.py:268): factories -> device bot ids
+        bot_ai = []
+        for f in ai2s:
+            d = f(None)
+            ai_id = getattr(d, "ai_id", None)
+            if ai_id is None:
+                raise MicroRTSNotImplemented(f"bot {d} has no device implementation")
+            bot_ai.append(ai_id)
+
+        # device + return contract
+        if device is None:
+            if not torch.cuda.is_available():
+                raise MicroRTSError("MicroRTSGridModeVecEnv needs a GPU (HIP) device: the engine has no CPU fallback")
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise MicroRTSError(f"device must be a HIP/cuda device, got {self.device}")
+        self.return_tensors = return_tensors
+        if obs_dtype is None:
+            obs_dtype = torch.float32 if return_tensors else torch.int32
+        if obs_dtype not in (torch.float32, torch.int32):
+            raise ValueError("obs_dtype must be torch.float32 or torch.int32")
+        self.obs_dtype = obs_dtype
+
+        # new JNIGridnetVecClient(...) (vec_env.py:256-276)
+        self._h = _native.create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, self._map_table, game_map,
+                                 bot_ai, _native.MRTS_OBS_FLOAT32 if obs_dtype == torch.float32 else _native.MRTS_OBS_INT32)
+        self._game_map = list(game_map)
+        info = _native.info(self._h)
+        assert (info.height, info.width) == (self.height, self.width)
+        self.utt = json.loads(_native.lib().mrts_utt_json(self._h).decode())
+        self.rfs = [RewardFunction(n) for n in RF_NAMES]
+        self.real_utt = self.utt
+        self.vec_client = self  # reference attribute; the client is the engine itself
+
+        with torch.cuda.device(self.device):
+            self._ws = torch.empty(int(info.workspace_bytes), dtype=torch.uint8, device=self.device)
+            hw = self.height * self.width
+            self.num_planes = [5, 5, 3, len(self.utt["unitTypes"]) + 1, 6, 2]
+            if partial_obs:
+                self.num_planes = [5, 5, 3, len(self.utt["unitTypes"]) + 1, 6, 2, 2]
+            P = sum(self.num_planes)
+            self._obs = torch.empty((self.num_envs, self.height, self.width, P), dtype=obs_dtype, device=self.device)
+            self._mask = torch.zeros((self.num_envs, hw, 78), dtype=torch.int32, device=self.device)
+            self._src = torch.zeros((self.num_envs, hw), dtype=torch.int32, device=self.device)
+            self._raw = torch.zeros((self.num_envs, 6), dtype=torch.float64, device=self.device)
+            self._done = torch.zeros((self.num_envs, 6), dtype=torch.uint8, device=self.device)
+            self._actions = torch.zeros((self.num_envs, hw, 7), dtype=torch.int64, device=self.device)
+            self._rw = torch.as_tensor(np.asarray(reward_weight, dtype=np.float64), device=self.device)
+        _native.check(_native.lib().mrts_bind_workspace(self._h, self._ws.data_ptr(), self._stream()), self._h, "bind_workspace")
+
+        # computed properties (vec_env.py:230-254)
+        self.action_space_dims = [6, 4, 4, 4, 4, len(self.utt["unitTypes"]), 7 * 7]
+        self.observation_space = Box(low=0.0, high=1.0, shape=(self.height, self.width, P), dtype=np.int32)
+        self.num_planes_len = len(self.num_planes)
+        self.num_planes_prefix_sum = [0]
+        for num_plane in self.num_planes:
+            self.num_planes_prefix_sum.append(self.num_planes_prefix_sum[-1] + num_plane)
+        self.action_space = MultiDiscrete(np.array([self.action_space_dims] * self.height * self.width).flatten())
+        self.action_plane_space = MultiDiscrete(self.action_space_dims)
+        self.source_unit_idxs = np.tile(np.arange(self.height * self.width), (self.num_envs, 1))
+        self.source_unit_idxs = self.source_unit_idxs.reshape((self.source_unit_idxs.shape + (1,)))
+        self._mask_valid = False
+        # optional {kernel name: [(start, end) torch.cuda.Event]} filled around
+        # each engine launch on the launch stream (bench.py roofline timing)
+        self.kernel_events = None
+
+    # ------------------------------------------------------------------ utils
+    def _launch(self, name, fn, *args):
+        ev = self.kernel_events
+        if ev is None:
+            rc = fn(*args)
+        else:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            rc = fn(*args)
+            e.record()
+            ev.setdefault(name, []).append((s, e))
+        _native.check(rc, self._h, name)
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _obs_out(self):
+        if self.return_tensors:
+            return self._obs
+        return self._obs.cpu().numpy()
+
+    # ------------------------------------------------------------------- API
+    def reset(self):
+        """vec_env.py:278-282"""
+        _native.check(_native.lib().mrts_reset(self._h, self._stream(), self._obs.data_ptr()), self._h, "reset")
+        self._mask_valid = False
+        return self._obs_out()
+
+    def get_action_mask(self):
+        """vec_env.py:1091-1101: (N, H*W, 78); channel 0 kept as source_unit_mask."""
+        self._launch("get_masks", _native.lib().mrts_get_masks, self._h, self._stream(), self._mask.data_ptr(), self._src.data_ptr())
+        self._mask_valid = True
+        if self.return_tensors:
+            return self._mask
+        return self._mask.cpu().numpy()
+
+    @property
+    def source_unit_mask(self):
+        return self._src if self.return_tensors else self._src.cpu().numpy()
+
+    def step_async(self, actions):
+        """vec_env.py:968-984: actions (N, H*W*7) (or any shape with N*H*W*7 elements)."""
+        hw = self.height * self.width
+        if isinstance(actions, torch.Tensor):
+            a = actions.reshape(self.num_envs, hw, 7)
+            if a.device == self.device and a.dtype == torch.int64 and a.is_contiguous():
+                self._actions_in = a
+                return
+            self._actions.copy_(a)
+        else:
+            a = np.asarray(actions).reshape(self.num_envs, hw, 7)
+            self._actions.copy_(torch.from_numpy(np.ascontiguousarray(a.astype(np.int64, copy=False))))
+        self._actions_in = self._actions
+
+    def step_wait(self):
+        """vec_env.py:1001-1057"""
+        if not self._mask_valid:
+            # the reference reads the source mask of the last get_action_mask
+            # (vec_env.py:974); compute it if the caller skipped that call
+            self.get_action_mask()
+        a = self._actions_in
+        self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
+                     self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
+        self._mask_valid = False
+        if self.return_tensors:
+            raw = self._raw
+            if not self.reward_shaping:
+                raw = raw.clone()
+                raw[:, 1:] = 0
+            done = self._done[:, 0].bool()
+            if len(self.cycle_maps) > 0:
+                self._cycle(done.cpu().numpy())
+            return self._obs, raw @ self._rw, done, LazyInfos(raw)
+        reward = self._raw.cpu().numpy()
+        done = self._done.cpu().numpy().astype(bool)
+        if not self.reward_shaping:
+            reward[:, 1:] = 0
+        if len(self.cycle_maps) > 0:
+            self._cycle(done[:, 0])
+        obs = self._obs.cpu().numpy()
+        infos = [{"raw_rewards": item} for item in reward]
+        return obs, reward @ self.reward_weight, done[:, 0], infos
+
+    def _cycle(self, done0):
+        """vec_env.py:1038-1056 map cycling, indexed the engine's way (selfplay
+        pairs first, then bot envs)."""
+        games, maps = [], []
+        nsp = self.num_selfplay_envs
+        for e in np.nonzero(done0)[0]:
+            if e < nsp:
+                if e % 2:
+                    continue
+                g = e // 2
+            else:
+                g = nsp // 2 + (e - nsp)
+            m = self._map_index[next(self.next_map)]
+            games.append(g)
+            maps.append(m)
+            self._game_map[g] = m
+        if games:
+            import ctypes
+
+            ga = (ctypes.c_int32 * len(games))(*games)
+            ma = (ctypes.c_int32 * len(maps))(*maps)
+            _native.check(
+                _native.lib().mrts_reset_games(self._h, self._stream(), ga, ma, len(games), self._obs.data_ptr()), self._h, "reset_games"
+            )
+
+    def step(self, ac):
+        self.step_async(ac)
+        return self.step_wait()
+
+    def getattr_depth_check(self, name, already_found):
+        """vec_env.py:1063-1073 (stable-baselines3 VecEnvWrapper protocol)."""
+        if hasattr(self, name) and already_found:
+            return "{0}.{1}".format(type(self).__module__, type(self).__name__)
+        return None
+
+    def render(self, mode="human"):
+        raise MicroRTSNotImplemented("render() (Java Swing / 640x640 RGB frames) is out of scope (DESIGN.md §8)")
+
+    def error_flags(self):
+        import ctypes
+
+        f = ctypes.c_int32(0)
+        _native.check(_native.lib().mrts_error_flags(self._h, self._stream(), ctypes.byref(f)), self._h, "error_flags")
+        return int(f.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            _native.lib().mrts_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

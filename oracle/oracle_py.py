@@ -1,0 +1,184 @@
+"""ctypes binding of the CPU restatement (oracle/libmrts_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package (microrts-py_amd/).
+
+OracleVecEnv mirrors the JNIGridnetVecClient + MicroRTSGridModeVecEnv pair of
+/root/reference/gym_microrts/envs/vec_env.py (reset 278-282, step_async/step_wait
+968-1057, get_action_mask 1091-1101) closely enough that the ported reference
+tests read the same against it.
+"""
+import ctypes
+import os
+import subprocess
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmrts_oracle.so")
+UNIT_TYPES = ["Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"]
+AI_IDS = {"passiveAI": 0, "workerRushAI": 1, "lightRushAI": 2, "randomBiasedAI": 3, "coacAI": 4}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.ovec_create.restype = P
+        L.ovec_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P]
+        L.ovec_destroy.argtypes = [P]
+        L.ovec_reset.argtypes = [P]
+        L.ovec_reset_game.argtypes = [P, ctypes.c_int, ctypes.c_int]
+        L.ovec_get_masks.argtypes = [P, P]
+        L.ovec_step.argtypes = [P, P, P, P, P]
+        L.ovec_raw_obs.argtypes = [P, P]
+        L.ovec_encode_obs.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+        L.ovec_game_time.argtypes = [P, ctypes.c_int]
+        L.ovec_game_time.restype = ctypes.c_int
+        L.ovec_game_resources.argtypes = [P, ctypes.c_int, P]
+        L.ovec_dump_cells.argtypes = [P, ctypes.c_int, P]
+        L.ovec_sample_actions.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P]
+        _lib = L
+    return _lib
+
+
+class _OMap(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("terrain", ctypes.c_void_p),
+        ("player_res", ctypes.c_int32 * 2),
+        ("num_units", ctypes.c_int32),
+        ("units", ctypes.c_void_p),
+    ]
+
+
+def parse_map(path):
+    """PhysicalGameState.load restated in Python (XML order kept)."""
+    root = ET.parse(path).getroot()
+    w, h = int(root.get("width")), int(root.get("height"))
+    terrain = np.array([int(ch) for ch in root.find("terrain").text.strip()], dtype=np.uint8)
+    assert terrain.size == w * h
+    res = [0, 0]
+    for p in root.find("players"):
+        res[int(p.get("ID"))] = int(p.get("resources"))
+    units = []
+    for u in root.find("units"):
+        units.append([UNIT_TYPES.index(u.get("type")), int(u.get("player")), int(u.get("x")), int(u.get("y")),
+                      int(u.get("resources")), int(u.get("hitpoints"))])
+    return {"width": w, "height": h, "terrain": terrain, "res": res, "units": np.array(units, dtype=np.int32).reshape(-1, 6)}
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleVecEnv:
+    """The oracle behind a MicroRTSGridModeVecEnv-shaped surface."""
+
+    def __init__(self, num_selfplay_envs, num_bot_envs, map_paths, max_steps=2000, partial_obs=False,
+                 ai2s=None, reward_weight=None, game_maps=None):
+        self.num_selfplay_envs, self.num_bot_envs = num_selfplay_envs, num_bot_envs
+        self.num_envs = num_selfplay_envs + num_bot_envs
+        self.num_games = num_selfplay_envs // 2 + num_bot_envs
+        self.partial_obs = partial_obs
+        self.maps = [parse_map(p) for p in map_paths]
+        self.height, self.width = self.maps[0]["height"], self.maps[0]["width"]
+        self._keep = []
+        arr = (_OMap * len(self.maps))()
+        for i, m in enumerate(self.maps):
+            arr[i].width, arr[i].height = m["width"], m["height"]
+            arr[i].terrain = ptr(m["terrain"])
+            arr[i].player_res[0], arr[i].player_res[1] = m["res"]
+            arr[i].num_units = len(m["units"])
+            arr[i].units = ptr(m["units"])
+        gm = np.zeros(self.num_games, np.int32) if game_maps is None else np.asarray(game_maps, np.int32)
+        ai = np.array([AI_IDS[a] if isinstance(a, str) else a for a in (ai2s or [0] * num_bot_envs)], np.int32)
+        if ai.size == 0:
+            ai = np.zeros(1, np.int32)
+        self._h = lib().ovec_create(num_selfplay_envs, num_bot_envs, max_steps, int(partial_obs),
+                                    ctypes.cast(arr, ctypes.c_void_p), len(self.maps), ptr(gm), ptr(ai))
+        self.reward_weight = np.asarray(reward_weight if reward_weight is not None else [10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+        hw = self.height * self.width
+        self.P_raw = 7 if partial_obs else 6
+        self.source_unit_mask = np.zeros((self.num_envs, hw), np.int32)
+
+    def close(self):
+        if self._h:
+            lib().ovec_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def raw_obs(self):
+        raw = np.zeros((self.num_envs, self.P_raw, self.height, self.width), np.int32)
+        lib().ovec_raw_obs(self._h, ptr(raw))
+        return raw
+
+    def encode(self, raw):
+        P = 31 if self.partial_obs else 29
+        out = np.zeros((raw.shape[0], self.height, self.width, P), np.int32)
+        lib().ovec_encode_obs(ptr(np.ascontiguousarray(raw)), raw.shape[0], self.height, self.width, int(self.partial_obs), ptr(out))
+        return out
+
+    def reset(self):
+        lib().ovec_reset(self._h)
+        return self.encode(self.raw_obs())
+
+    def reset_game(self, game, map_id):
+        lib().ovec_reset_game(self._h, game, map_id)
+
+    def get_action_mask_full(self):
+        m = np.zeros((self.num_envs, self.height * self.width, 79), np.int32)
+        lib().ovec_get_masks(self._h, ptr(m))
+        return m
+
+    def get_action_mask(self):
+        m = self.get_action_mask_full()
+        self.source_unit_mask = np.ascontiguousarray(m[:, :, 0])
+        return np.ascontiguousarray(m[:, :, 1:])
+
+    def step_raw(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions).reshape(self.num_envs, self.height * self.width, 7).astype(np.int64))
+        reward = np.zeros((self.num_envs, 6), np.float64)
+        done = np.zeros((self.num_envs, 6), np.uint8)
+        lib().ovec_step(self._h, ptr(a), ptr(self.source_unit_mask), ptr(reward), ptr(done))
+        return reward, done.astype(bool)
+
+    def step(self, actions):
+        reward, done = self.step_raw(actions)
+        obs = self.encode(self.raw_obs())
+        infos = [{"raw_rewards": r} for r in reward]
+        return obs, reward @ self.reward_weight, done[:, 0], infos
+
+    def game_time(self, g):
+        return lib().ovec_game_time(self._h, g)
+
+    def game_resources(self, g):
+        r = np.zeros(2, np.int32)
+        lib().ovec_game_resources(self._h, g, ptr(r))
+        return r
+
+    def dump_cells(self, g):
+        out = np.zeros((self.height * self.width, 8), np.int32)
+        lib().ovec_dump_cells(self._h, g, ptr(out))
+        return out
+
+
+def sample_actions(masks78, seed, step):
+    """Philox-keyed masked sampler (same stream as the GPU bench sampler)."""
+    m = np.ascontiguousarray(masks78, dtype=np.int32)
+    n, hw = m.shape[0], m.shape[1]
+    out = np.zeros((n, hw, 7), np.int64)
+    lib().ovec_sample_actions(ptr(m), n, hw, ctypes.c_uint64(seed), ctypes.c_uint32(step), ptr(out))
+    return out

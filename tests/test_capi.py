@@ -1,0 +1,113 @@
+"""The drop-in boundary on CPU: libmicrorts_amd.so loads, exports every entry
+point include/microrts_amd.h declares, and its host-only calls (config
+validation, map XML loading, unit-type JSON) behave -- no kernel launches."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import MAPS, REPO
+
+HEADER = os.path.join(REPO, "include", "microrts_amd.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(mrts_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_api():
+    syms = declared_symbols()
+    for s in ["mrts_create", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_destroy", "mrts_last_error"]:
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from gym_microrts import _native
+
+    L = _native.lib()
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(_native.SIGNATURES) == set(declared_symbols())
+
+
+def _create(**kw):
+    from gym_microrts import _native
+
+    args = dict(num_selfplay_envs=4, num_bot_envs=2, max_steps=2000, partial_obs=False,
+                map_paths=[os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml")], game_map=[0, 0, 0, 0], bot_ai=[0, 0],
+                obs_dtype=1)
+    args.update(kw)
+    return _native.create(**args)
+
+
+def test_create_and_info():
+    from gym_microrts import _native
+
+    h = _create()
+    i = _native.info(h)
+    assert (i.height, i.width, i.num_envs, i.num_games, i.obs_planes, i.mask_channels) == (16, 16, 6, 4, 29, 78)
+    assert i.workspace_bytes >= 4 * 256 * 16
+    utt = json.loads(_native.lib().mrts_utt_json(h).decode())
+    names = [u["name"] for u in utt["unitTypes"]]
+    assert names == ["Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"]
+    assert len(utt["unitTypes"]) + 1 == 8   # num_planes unit-type group (vec_env.py:235)
+    _native.lib().mrts_destroy(h)
+
+
+@pytest.mark.parametrize("kw,err", [
+    (dict(num_selfplay_envs=3), "MicroRTSError"),
+    (dict(max_steps=0), "MicroRTSError"),
+    (dict(map_paths=["/nonexistent.xml"]), "MicroRTSError"),
+    (dict(bot_ai=[4, 0]), "MicroRTSNotImplemented"),
+    (dict(partial_obs=True), "MicroRTSNotImplemented"),
+])
+def test_create_rejects_bad_config(kw, err):
+    from gym_microrts import _native
+
+    with pytest.raises(getattr(_native, err)):
+        _create(**kw)
+
+
+def test_mixed_map_sizes_rejected():
+    with pytest.raises(Exception, match="share height"):
+        _create(map_paths=[os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml"), os.path.join(MAPS, "maps/8x8/basesWorkers8x8.xml")])
+
+
+def test_unbound_calls_fail_loudly():
+    from gym_microrts import _native
+
+    h = _create()
+    rc = _native.lib().mrts_reset(h, None, ctypes.c_void_p(16))
+    assert rc != 0 and b"not bound" in _native.lib().mrts_last_error(h)
+
+
+def test_map_loader_matches_python_parser():
+    """C++ PhysicalGameState loader vs the oracle harness' python parser on every
+    authored map: same size and unit count (workspace size reflects maps)."""
+    from gym_microrts import _native
+    from oracle_py import parse_map
+
+    for root, _, files in os.walk(os.path.join(MAPS, "maps")):
+        for f in files:
+            p = os.path.join(root, f)
+            m = parse_map(p)
+            h = _native.create(2, 0, 100, False, [p], [0], [], 1)
+            i = _native.info(h)
+            assert (i.height, i.width) == (m["height"], m["width"])
+            _native.lib().mrts_destroy(h)
+            assert len(m["units"]) > 0 and np.all(m["units"][:, 5] >= 1)
+
+
+def test_env_requires_gpu_when_absent():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+
+    with pytest.raises(RuntimeError, match="GPU"):
+        MicroRTSGridModeVecEnv(num_selfplay_envs=2, num_bot_envs=0, map_paths=["maps/16x16/basesWorkers16x16.xml"])
