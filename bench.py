@@ -52,8 +52,27 @@ def kernel_bytes(G, N, HW, P=29):
            + raw reward (48 B/env) + done (6 B/env); action rows (56 B per acting unit) not counted."""
     return {
         "get_masks": G * HW * 16 + N * HW * (78 * 4 + 4),
-        "step": G * HW * 32 + N * HW * (4 + 4 * P) + N * (48 + 6),
+        "step": G * HW * 32 + N * HW * (4 + 4 * P) + N * (48 + 6 + 8 + 1),
+        "sample": N * HW * (78 * 4 + 7 * 8),
     }
+
+
+# rocprofv3 kernel names -> bench kernel names
+PMC_NAMES = {"get_masks": "k_masks", "step": "k_step", "sample": "k_sample"}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_latest.json, written by scripts/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command)."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    for k, v in d.items():
+        if k.startswith(PMC_NAMES.get(kernel, "?")) and v.get("hbm_bytes"):
+            return v["hbm_bytes"], "profiles/pmc_latest.json"
+    return None, None
 
 
 def run_gpu(args, rank, world, local_rank):
@@ -187,9 +206,12 @@ def main():
         dom = max((k for k in kern if k in kb), key=lambda k: kern[k], default=None)
         if dom:
             achieved = kb[dom] / (kern[dom] * 1e-3) / 1e9
+            traffic, tsrc = pmc_traffic(dom)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                    "avg_launch_ms": round(kern[dom], 4)}
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None if traffic is None else round(traffic / (kern[dom] * 1e-3) / 1e9, 1),
+                    "traffic_bytes_per_launch": traffic, "traffic_source": tsrc,
+                    "algorithmic_bytes_per_launch": kb[dom], "kernel": dom, "avg_launch_ms": round(kern[dom], 4)}
         env_step_bytes = hw * (4 * 29 + 312 + 56 + 32) + 64   # SURVEY.md §8d whole-step formula
         out = {
             "metric": METRIC,

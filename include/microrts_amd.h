@@ -96,6 +96,17 @@ int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source);
 int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source,
               void *obs, double *raw_reward, uint8_t *done);
 
+/* reward_weight and reward_shaping of MicroRTSGridModeVecEnv (vec_env.py:102-103,
+ * 1003-1004, 1057), used by mrts_step_weighted.  Host array of 6 doubles. */
+int mrts_set_reward_weight(mrts_vec *h, const double *weight6, int32_t reward_shaping);
+
+/* mrts_step + the step_wait reduction fused into the same kernel
+ * (vec_env.py:1003-1004, 1057): reward [N] float64 = raw_reward @ weight
+ * (k = 0..5 in order, round-to-nearest, no FMA; channels 1..5 taken as 0 when
+ * reward_shaping is off) and done0 [N] uint8 = done[:, 0]. */
+int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs,
+                       double *raw_reward, uint8_t *done, double *reward, uint8_t *done0);
+
 /* Map cycling (vec_env.py:1038-1056): reset `count` games (host arrays) onto
  * the given map indices and rewrite their envs' obs. */
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);

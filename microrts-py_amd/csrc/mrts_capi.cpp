@@ -161,6 +161,8 @@ struct mrts_vec {
     unsigned char *ws = nullptr;
     std::vector<int32_t> scratch_host;
     std::string err, utt;
+    double rw[6] = {0, 0, 0, 0, 0, 0};
+    int shaping = 1;
     EngineParams base{};
 };
 
@@ -318,6 +320,31 @@ int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *
     p.obs = obs;
     p.raw_reward = raw_reward;
     p.done = done;
+    hipError_t e = mrts_engine_step(&p, (hipStream_t)stream);
+    return e ? hip_fail(h, e, "step launch") : MRTS_OK;
+}
+
+int mrts_set_reward_weight(mrts_vec *h, const double *w, int32_t shaping) {
+    if (!h || !w) return fail(h, MRTS_EINVAL, "set_reward_weight: null argument");
+    for (int k = 0; k < 6; k++) h->rw[k] = w[k];
+    h->shaping = shaping ? 1 : 0;
+    return MRTS_OK;
+}
+
+int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs,
+                       double *raw_reward, uint8_t *done, double *reward, uint8_t *done0) {
+    if (!bound(h) || !actions || !source || !obs || !raw_reward || !done || !reward || !done0)
+        return fail(h, MRTS_ESTATE, "step_weighted: workspace not bound or null buffer");
+    EngineParams p = h->base;
+    p.actions = actions;
+    p.src = source;
+    p.obs = obs;
+    p.raw_reward = raw_reward;
+    p.done = done;
+    p.reward = reward;
+    p.done0 = done0;
+    for (int k = 0; k < 6; k++) p.rw[k] = h->rw[k];
+    p.shaping = h->shaping;
     hipError_t e = mrts_engine_step(&p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
 }

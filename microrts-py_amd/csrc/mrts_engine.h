@@ -20,6 +20,12 @@ struct EngineParams {
     uint8_t *done;          // [N][6]
     int32_t *mask;          // [N][HW][78]
     int32_t *src_out;       // [N][HW]
+    // optional fused step_wait outputs (vec_env.py:1057): reward = raw @ rw
+    // (float64, k = 0..5 in order; channels 1..5 zeroed when !shaping) and done[:,0]
+    double *reward;         // [N] or null
+    uint8_t *done0;         // [N] or null (torch.bool storage)
+    double rw[6];
+    int shaping;
 };
 
 extern "C" {

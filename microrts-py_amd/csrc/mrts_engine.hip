@@ -807,6 +807,16 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         p.raw_reward[(size_t)env * 6 + k] = r;
         p.done[(size_t)env * 6 + k] = (uint8_t)((gameover || (k == 0 && reset)) ? 1 : 0);
     }
+    if (p.reward && threadIdx.x < G.nviews) {   // fused `reward @ reward_weight`, done[:, 0]
+        const int v = threadIdx.x, env = G.env0 + v;
+        double s = 0.0;
+        for (int k = 0; k < 6; k++) {
+            double r = k == 0 ? (gameover ? (winner == v ? 1.0 : -1.0) : 0.0) : (p.shaping ? (double)L.sc[SC_R0 + 6 * v + k] : 0.0);
+            s = __dadd_rn(s, __dmul_rn(r, p.rw[k]));   // no FMA contraction: numpy's sequential dot
+        }
+        p.reward[env] = s;
+        p.done0[env] = (uint8_t)(reset ? 1 : 0);
+    }
     __syncthreads();
     if (reset) {
         reset_into_lds<NT>(p, L, L.sc[SC_MAP]);
@@ -836,52 +846,81 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
     }
 }
 
-__global__ __launch_bounds__(256) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed, uint32_t step,
-                                                int64_t* __restrict__ act) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= n * hw) return;
-    const int e = idx / hw, c = idx - e * hw;
-    // 78 int32 = 39 x 8-byte loads (rows are 312 B, 8-byte aligned)
-    const int2* m2 = reinterpret_cast<const int2*>(mask + (size_t)idx * MRTS_MASK_CH);
-    uint32_t bits[3] = {0, 0, 0};
+// One workgroup = SR consecutive (env, cell) rows.  The rows' 78-int32 masks
+// (SR*312 B, contiguous) are streamed with coalesced 16-byte loads and folded
+// into 78-bit words in LDS; each lane then samples its row and the 7 int64
+// components are staged in LDS and written back with coalesced 16-byte stores.
+constexpr int SR = 256;
+
+__global__ __launch_bounds__(SR) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed, uint32_t step,
+                                               int64_t* __restrict__ act) {
+    __shared__ uint32_t s_bits[SR * 3];
+    __shared__ __attribute__((aligned(16))) int64_t s_out[SR * 7];
+    const long long rows = (long long)n * hw;
+    const long long row0 = (long long)blockIdx.x * SR;
+    const int rb = (int)min((long long)SR, rows - row0);
+    for (int i = threadIdx.x; i < SR * 3; i += SR) s_bits[i] = 0;
+    __syncthreads();
+    const int32_t* mb = mask + row0 * MRTS_MASK_CH;   // 16-B aligned: SR*312 B per block
+    const int nel = rb * MRTS_MASK_CH, nv = nel >> 2;
+    const int4* m4 = reinterpret_cast<const int4*>(mb);
+    for (int k = threadIdx.x; k < nv; k += SR) {
+        int4 v = m4[k];
+        if ((v.x | v.y | v.z | v.w) == 0) continue;   // most cells hold no idle unit
+        int e = 4 * k;
+        int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
+        int vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int j = 0; j < MRTS_MASK_CH / 2; j++) {
-        int2 v = m2[j];
-        int b = 2 * j;
-        if (v.x) bits[b >> 5] |= 1u << (b & 31);
-        if (v.y) bits[(b + 1) >> 5] |= 1u << ((b + 1) & 31);
-    }
-    uint32_t r[8];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
-        philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-        r[4 * h] = ctr[0]; r[4 * h + 1] = ctr[1]; r[4 * h + 2] = ctr[2]; r[4 * h + 3] = ctr[3];
-    }
-    const int off[7] = {0, 6, 10, 14, 18, 22, 29};
-    const int len[7] = {6, 4, 4, 4, 4, 7, 49};
-    int64_t out[7];
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        int nvalid = 0;
-        for (int j = 0; j < len[k]; j++) nvalid += (bits[(off[k] + j) >> 5] >> ((off[k] + j) & 31)) & 1u;
-        int pick = 0;
-        if (nvalid == 0) {
-            pick = (int)(((uint64_t)r[k] * (uint32_t)len[k]) >> 32);
-        } else {
-            int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
-            for (int j = 0; j < len[k]; j++) {
-                if ((bits[(off[k] + j) >> 5] >> ((off[k] + j) & 31)) & 1u) {
-                    if (t == 0) { pick = j; break; }
-                    t--;
-                }
-            }
+        for (int j = 0; j < 4; j++) {
+            if (vv[j]) atomicOr(&s_bits[3 * r + (ch >> 5)], 1u << (ch & 31));
+            if (++ch == MRTS_MASK_CH) { ch = 0; r++; }
         }
-        out[k] = pick;
     }
-    int64_t* o = act + (size_t)idx * 7;
+    for (int e = 4 * nv + threadIdx.x; e < nel; e += SR) {
+        if (mb[e]) {
+            int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
+            atomicOr(&s_bits[3 * r + (ch >> 5)], 1u << (ch & 31));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < rb) {
+        const long long idx = row0 + threadIdx.x;
+        const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
+        const uint64_t lo = (uint64_t)s_bits[3 * threadIdx.x] | ((uint64_t)s_bits[3 * threadIdx.x + 1] << 32);
+        const uint64_t hi = s_bits[3 * threadIdx.x + 2];
+        uint32_t r[8];
 #pragma unroll
-    for (int k = 0; k < 7; k++) o[k] = out[k];
+        for (int h = 0; h < 2; h++) {
+            uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
+            philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+            r[4 * h] = ctr[0]; r[4 * h + 1] = ctr[1]; r[4 * h + 2] = ctr[2]; r[4 * h + 3] = ctr[3];
+        }
+        const int off[7] = {0, 6, 10, 14, 18, 22, 29};
+        const int len[7] = {6, 4, 4, 4, 4, 7, 49};
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            // segment bits [off, off+len) of the 78-bit word
+            uint64_t seg = (lo >> off[k]) | (off[k] ? (hi << (64 - off[k])) : 0);
+            seg &= (1ull << len[k]) - 1ull;
+            const int nvalid = __popcll(seg);
+            int pick;
+            if (nvalid == 0) {
+                pick = (int)(((uint64_t)r[k] * (uint32_t)len[k]) >> 32);
+            } else {
+                int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
+                for (; t > 0; t--) seg &= seg - 1ull;   // drop the t lowest set bits
+                pick = __builtin_ctzll(seg);
+            }
+            s_out[threadIdx.x * 7 + k] = pick;
+        }
+    }
+    __syncthreads();
+    int64_t* ob = act + row0 * 7;   // 16-B aligned: SR*56 B per block
+    const int onel = rb * 7, onv = onel >> 1;
+    int4* o4 = reinterpret_cast<int4*>(ob);
+    const int4* s4 = reinterpret_cast<const int4*>(s_out);
+    for (int k = threadIdx.x; k < onv; k += SR) o4[k] = s4[k];
+    if ((onel & 1) && threadIdx.x == 0) ob[onel - 1] = s_out[onel - 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -921,7 +960,7 @@ hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts:
 hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
     int total = n * hw;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(mrts::k_sample, dim3((total + 255) / 256), dim3(256), 0, s, mask, n, hw, seed, step, act);
+    hipLaunchKernelGGL(mrts::k_sample, dim3((total + mrts::SR - 1) / mrts::SR), dim3(mrts::SR), 0, s, mask, n, hw, seed, step, act);
     return hipGetLastError();
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {

@@ -212,8 +212,11 @@ class MicroRTSGridModeVecEnv:
             self._raw = torch.zeros((self.num_envs, 6), dtype=torch.float64, device=self.device)
             self._done = torch.zeros((self.num_envs, 6), dtype=torch.uint8, device=self.device)
             self._actions = torch.zeros((self.num_envs, hw, 7), dtype=torch.int64, device=self.device)
-            self._rw = torch.as_tensor(np.asarray(reward_weight, dtype=np.float64), device=self.device)
+            self._rew = torch.zeros((self.num_envs,), dtype=torch.float64, device=self.device)
+            self._done0 = torch.zeros((self.num_envs,), dtype=torch.bool, device=self.device)
         _native.check(_native.lib().mrts_bind_workspace(self._h, self._ws.data_ptr(), self._stream()), self._h, "bind_workspace")
+        rw = np.ascontiguousarray(np.asarray(reward_weight, dtype=np.float64).reshape(6))
+        _native.check(_native.lib().mrts_set_reward_weight(self._h, rw.ctypes.data, int(bool(reward_shaping))), self._h, "set_reward_weight")
 
         # computed properties (vec_env.py:230-254)
         self.action_space_dims = [6, 4, 4, 4, 4, len(self.utt["unitTypes"]), 7 * 7]
@@ -291,18 +294,21 @@ class MicroRTSGridModeVecEnv:
             # (vec_env.py:974); compute it if the caller skipped that call
             self.get_action_mask()
         a = self._actions_in
-        self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
-                     self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
         self._mask_valid = False
         if self.return_tensors:
+            # reward @ reward_weight and done[:, 0] are fused into the step kernel
+            self._launch("step", _native.lib().mrts_step_weighted, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
+                         self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr(), self._rew.data_ptr(),
+                         self._done0.data_ptr())
             raw = self._raw
             if not self.reward_shaping:
                 raw = raw.clone()
                 raw[:, 1:] = 0
-            done = self._done[:, 0].bool()
             if len(self.cycle_maps) > 0:
-                self._cycle(done.cpu().numpy())
-            return self._obs, raw @ self._rw, done, LazyInfos(raw)
+                self._cycle(self._done0.cpu().numpy())
+            return self._obs, self._rew, self._done0, LazyInfos(raw)
+        self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
+                     self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
         reward = self._raw.cpu().numpy()
         done = self._done.cpu().numpy().astype(bool)
         if not self.reward_shaping:

@@ -102,7 +102,16 @@ def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_
         np.testing.assert_array_equal(obs_g, obs_o, err_msg=f"obs step {s}")
         np.testing.assert_array_equal(np.array([i["raw_rewards"] for i in info_g]), np.array([i["raw_rewards"] for i in info_o]),
                                       err_msg=f"raw rewards step {s}")
-        np.testing.assert_array_equal(rew_g, rew_o, err_msg=f"weighted reward step {s}")
+        if return_tensors:
+            # fused in-kernel dot: sequential k = 0..5, round-to-nearest, no FMA
+            raw_o = np.array([i["raw_rewards"] for i in info_o])
+            seq = np.zeros(n)
+            for k in range(6):
+                seq = seq + raw_o[:, k] * g.reward_weight[k]
+            np.testing.assert_array_equal(rew_g, seq, err_msg=f"weighted reward step {s}")
+            np.testing.assert_allclose(rew_g, rew_o, rtol=0, atol=1e-12)   # vs numpy `raw @ w`
+        else:
+            np.testing.assert_array_equal(rew_g, rew_o, err_msg=f"weighted reward step {s}")
         np.testing.assert_array_equal(done_g, done_o, err_msg=f"done step {s}")
         episodes += int(np.asarray(done_o).sum())
     assert g.error_flags() == 0
@@ -156,6 +165,25 @@ def test_device_sampler_matches_oracle_sampler():
                                                         ctypes.c_uint64(0xDEADBEEF12345678), step, out.data_ptr()))
         ref = sample_actions(m.cpu().numpy(), 0xDEADBEEF12345678, step)
         np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("rows", [1, 37, 255, 256, 257, 1000])
+def test_device_sampler_ragged_rows(rows):
+    """Blocks of 256 rows: partial last block, odd element / int64 tails."""
+    import ctypes
+
+    from gym_microrts import _native
+    from oracle_py import sample_actions
+
+    torch = _torch()
+    rng = np.random.default_rng(rows)
+    m = (rng.random((1, rows, 78)) < 0.2).astype(np.int32)
+    m[0, ::3] = 0   # rows with no valid entry use the uniform fallback
+    md = torch.from_numpy(m).cuda()
+    out = torch.full((1, rows, 7), -1, dtype=torch.int64, device="cuda")
+    _native.check(_native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, md.data_ptr(), 1, rows,
+                                                    ctypes.c_uint64(42), 7, out.data_ptr()))
+    np.testing.assert_array_equal(out.cpu().numpy(), sample_actions(m, 42, 7))
 
 
 def test_map_cycling_matches_oracle():
