@@ -189,7 +189,6 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     if (cfg->num_selfplay_envs + cfg->num_bot_envs <= 0) return fail(h, MRTS_EINVAL, "no envs");
     if (cfg->max_steps <= 0 || cfg->max_steps >= MRTS_MAX_TIME)
         return fail(h, MRTS_EINVAL, "max_steps must be in [1, 500000)");
-    if (cfg->partial_obs) return fail(h, MRTS_ENOTIMPL, "partial_obs is not implemented yet (DESIGN.md §8)");
     if (cfg->num_maps <= 0 || !cfg->map_paths) return fail(h, MRTS_EINVAL, "no maps");
     h->nsp = cfg->num_selfplay_envs;
     h->nbot = cfg->num_bot_envs;
@@ -287,6 +286,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.nsp_games = h->nsp / 2;
     p.max_steps = h->max_steps;
     p.obs_float = h->obs_float;
+    p.partial_obs = h->partial_obs;
     h->err.clear();
     return MRTS_OK;
 }

@@ -12,7 +12,7 @@ struct EngineParams {
     const uint8_t *map_wall;// [maps][HW]
     const int32_t *map_scal;// [maps][MRTS_MAP_SCALARS]
     int G, HW, W, H;
-    int nsp, nsp_games, max_steps, obs_float;
+    int nsp, nsp_games, max_steps, obs_float, partial_obs;
     const int64_t *actions; // [N][HW][7]
     const int32_t *src;     // [N][HW]
     void *obs;              // [N][HW][P]

@@ -42,6 +42,9 @@ __device__ __forceinline__ int ut_attack_time(int t) { return t >= WORKER ? 5 : 
 __device__ __forceinline__ int ut_harvest_time(int t) { return t == WORKER ? 20 : 10; }
 __device__ __forceinline__ int ut_return_time(int) { return 10; }
 __device__ __forceinline__ int ut_harvest_amount(int) { return 1; }
+__device__ __forceinline__ int ut_sight(int t) {
+    return t == BASE ? 5 : (t == BARRACKS || t == WORKER || t == RANGED) ? 3 : (t == LIGHT || t == HEAVY) ? 2 : 0;
+}
 __device__ __forceinline__ bool ut_can_move(int t) { return t >= WORKER; }
 __device__ __forceinline__ bool ut_can_attack(int t) { return t >= WORKER; }
 __device__ __forceinline__ bool ut_can_harvest(int t) { return t == WORKER; }
@@ -211,16 +214,22 @@ __device__ void cell_mask(const Grid& gd, int c, int player, const uint32_t* s_u
     }
 }
 
-// one-hot word of vec_env.py:311-321 for the cell (perspective `player`)
-__device__ __forceinline__ uint32_t cell_onehot(uint32_t u, uint32_t a, uint8_t wall, int player) {
+// one-hot word of vec_env.py:311-321 for the cell (perspective `player`).
+// Partial observability (P == 31, PartiallyObservableGameState): `shown` is 0
+// for a unit the player cannot see (the cell reads as empty); bits 29/30 are
+// the visibility plane: the shown unit is visible to the opponent.
+__device__ __forceinline__ uint32_t cell_onehot(uint32_t u, uint32_t a, uint8_t wall, int player, int P = 29,
+                                                bool shown = true, bool opp_sees = false) {
     uint32_t b = 0;
+    if (!shown) u = 0;
+    if (P == 31) b |= 1u << (29 + ((u != 0 && opp_sees) ? 1 : 0));
     if (u == 0) {
-        b = 1u | (1u << 5) | (1u << 10) | (1u << 13) | (1u << 21);
+        b |= 1u | (1u << 5) | (1u << 10) | (1u << 13) | (1u << 21);
     } else {
         int hp = min(max(u_hp(u), 0), 4), res = min(u_res(u), 4), ow = u_owner(u);
         int rel = ow < 0 ? 0 : (ow == player ? 1 : 2);
         int at = a ? min(code_type(act_code(a)), 5) : 0;
-        b = (1u << hp) | (1u << (5 + res)) | (1u << (10 + rel)) | (1u << (13 + u_type(u) + 1)) | (1u << (21 + at));
+        b |= (1u << hp) | (1u << (5 + res)) | (1u << (10 + rel)) | (1u << (13 + u_type(u) + 1)) | (1u << (21 + at));
     }
     return b | (1u << (27 + (wall ? 1 : 0)));
 }
@@ -241,6 +250,7 @@ struct Lds {
     uint8_t* wall;
     unsigned long long* ballot;
     uint32_t* posbits;
+    uint32_t* vis;   // [2][HW/32+1] cells observable by player 0 / 1 (partial obs)
     int* sc;         // scalars
 };
 enum { SC_TIME = 0, SC_RES0, SC_RES1, SC_UID, SC_STEPS, SC_MAP, SC_ERR, SC_NPROD, SC_CNT, SC_GO, SC_WIN,
@@ -257,6 +267,7 @@ __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     b += a16(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     b += a16(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     b += a16(4 * SC_WORDS);
+    b += a16(8 * (size_t)(HW / 32 + 1));
     return b;
 }
 
@@ -279,6 +290,7 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     L.ballot = (unsigned long long*)take(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     L.posbits = (uint32_t*)take(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     L.sc = (int*)take(4 * SC_WORDS);
+    L.vis = (uint32_t*)take(8 * (size_t)(HW / 32 + 1));
     return L;
 }
 
@@ -372,10 +384,50 @@ __device__ void store_game(const EngineParams& p, const Lds& L, int g) {
 }
 
 // write the one-hot observation of one view: bits in L.aux, 16-byte stores
+// PartiallyObservableGameState.observable for both players: a cell is seen by
+// player q when some unit of q is within its sight radius (d^2 <= r^2).  Each
+// unit lane ORs its sight disk into the player's LDS bitmap.
+template <int NT>
+__device__ void compute_vis(const EngineParams& p, const Lds& L) {
+    const int HW = p.HW, nw = HW / 32 + 1;
+    for (int i = threadIdx.x; i < 2 * nw; i += NT) L.vis[i] = 0;
+    __syncthreads();
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        uint32_t u = L.unit[c];
+        int q = u_owner(u);
+        if (u == 0 || q < 0) continue;
+        int r = ut_sight(u_type(u)), x = c % p.W, y = c / p.W;
+        uint32_t* vq = L.vis + q * nw;
+        for (int dy = -r; dy <= r; dy++) {
+            int yy = y + dy;
+            if (yy < 0 || yy >= p.H) continue;
+            for (int dx = -r; dx <= r; dx++) {
+                int xx = x + dx;
+                if (xx < 0 || xx >= p.W || dx * dx + dy * dy > r * r) continue;
+                int cc = yy * p.W + xx;
+                atomicOr(&vq[cc >> 5], 1u << (cc & 31));
+            }
+        }
+    }
+    __syncthreads();
+}
+
 template <int NT, int P, typename OT>
 __device__ void write_obs(const EngineParams& p, const Lds& L, int env, int player) {
     const int HW = p.HW;
-    for (int c = threadIdx.x; c < HW; c += NT) L.aux[c] = cell_onehot(L.unit[c], L.act[c], L.wall[c], player);
+    if (P == 31) {
+        const int nw = HW / 32 + 1;
+        const uint32_t* vme = L.vis + player * nw;
+        const uint32_t* vop = L.vis + (1 - player) * nw;
+        for (int c = threadIdx.x; c < HW; c += NT) {
+            uint32_t u = L.unit[c];
+            bool shown = u == 0 || u_owner(u) == player || ((vme[c >> 5] >> (c & 31)) & 1u);
+            bool opp = (vop[c >> 5] >> (c & 31)) & 1u;
+            L.aux[c] = cell_onehot(u, L.act[c], L.wall[c], player, P, shown, opp);
+        }
+    } else {
+        for (int c = threadIdx.x; c < HW; c += NT) L.aux[c] = cell_onehot(L.unit[c], L.act[c], L.wall[c], player);
+    }
     __syncthreads();
     OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)env * HW * P;
     const int total = HW * P;
@@ -415,6 +467,7 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
     __syncthreads();
     store_game<NT>(p, L, g);
     Game G = game_of(p, g);
+    if (P == 31) compute_vis<NT>(p, L);
     for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
 }
 
@@ -827,6 +880,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     __syncthreads();
     // (7) write back + one-hot observation of every view
     store_game<NT>(p, L, g);
+    if (P == 31) compute_vis<NT>(p, L);
     for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
 }
 
@@ -932,13 +986,23 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
     if (kind == 0) {   // reset
         grid = games ? count : p.G;
         if (grid == 0) return hipSuccess;
-        if (p.obs_float) hipLaunchKernelGGL((k_reset<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
-        else hipLaunchKernelGGL((k_reset<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+        if (p.partial_obs) {
+            if (p.obs_float) hipLaunchKernelGGL((k_reset<NT, 31, float>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+            else hipLaunchKernelGGL((k_reset<NT, 31, int32_t>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+        } else {
+            if (p.obs_float) hipLaunchKernelGGL((k_reset<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+            else hipLaunchKernelGGL((k_reset<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p, games, maps, count);
+        }
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
     } else {
-        if (p.obs_float) hipLaunchKernelGGL((k_step<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p);
-        else hipLaunchKernelGGL((k_step<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+        if (p.partial_obs) {
+            if (p.obs_float) hipLaunchKernelGGL((k_step<NT, 31, float>), dim3(grid), dim3(NT), sh, s, p);
+            else hipLaunchKernelGGL((k_step<NT, 31, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+        } else {
+            if (p.obs_float) hipLaunchKernelGGL((k_step<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p);
+            else hipLaunchKernelGGL((k_step<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+        }
     }
     return hipGetLastError();
 }

@@ -650,7 +650,24 @@ static void rewards(const OGS *g, const OPA *pa0, const OPA *pa1, int maxplayer,
     for (int i = 0; i < 6; i++) d[i] = (uint8_t)(gameover ? 1 : 0);
 }
 
-/* GameState.getVectorObservation(player) (+ visibility plane with partial obs) */
+/* PartiallyObservableGameState.observable(x, y) for `player`: some unit of the
+ * player has sqrt(dx^2 + dy^2) <= sightRadius (README.md:90-92; UNPINNED,
+ * DESIGN.md §4).                                                            */
+static int observable(const OGS *g, int player, int x, int y) {
+    for (int i = 0; i < g->nu; i++) {
+        const OUnit *u = &g->u[i];
+        if (!u->alive || u->player != player) continue;
+        int dx = u->x - x, dy = u->y - y;
+        if (dx * dx + dy * dy <= UT[u->type].sight * UT[u->type].sight) return 1;
+    }
+    return 0;
+}
+
+/* GameState.getVectorObservation(player).  With partial obs the observation is
+ * that of new PartiallyObservableGameState(gs, player) -- every unit not owned
+ * by the player (resources included) that the player cannot observe is
+ * removed -- plus raw plane 6: the shown unit is observable by the opponent
+ * (README.md:90-92 "visible to the opponent"; 0 on empty cells).            */
 static void vector_obs(const OGS *g, int player, int partial, int32_t *raw) {
     int HW = g->W * g->H;
     int P = partial ? 7 : 6;
@@ -659,14 +676,15 @@ static void vector_obs(const OGS *g, int player, int partial, int32_t *raw) {
     for (int i = 0; i < g->nu; i++) {
         const OUnit *u = &g->u[i];
         if (!u->alive) continue;
+        if (partial && u->player != player && !observable(g, player, u->x, u->y)) continue;
         int c = u->y * g->W + u->x;
+        if (partial) raw[6 * HW + c] = observable(g, 1 - player, u->x, u->y);
         raw[0 * HW + c] = u->hp;
         raw[1 * HW + c] = u->res;
         raw[2 * HW + c] = u->player < 0 ? 0 : (u->player == player ? 1 : 2);
         raw[3 * HW + c] = u->type + 1;
         raw[4 * HW + c] = u->assign >= 0 ? g->as[u->assign].act.type : A_NONE;
     }
-    (void)partial; /* partial observability: DESIGN.md §8 (next) */
 }
 
 /* JNIGridnetClient.getMasks(player) -> [HW][79] */

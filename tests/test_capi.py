@@ -63,7 +63,7 @@ def test_create_and_info():
     (dict(max_steps=0), "MicroRTSError"),
     (dict(map_paths=["/nonexistent.xml"]), "MicroRTSError"),
     (dict(bot_ai=[4, 0]), "MicroRTSNotImplemented"),
-    (dict(partial_obs=True), "MicroRTSNotImplemented"),
+    (dict(bot_ai=[99, 0]), "MicroRTSError"),
 ])
 def test_create_rejects_bad_config(kw, err):
     from gym_microrts import _native

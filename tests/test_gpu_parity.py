@@ -39,12 +39,12 @@ def make_gpu_env(num_selfplay_envs, num_bot_envs, map_path, max_steps, reward_we
     )
 
 
-def make_oracle(num_selfplay_envs, num_bot_envs, map_path, max_steps, maps=None, game_maps=None):
+def make_oracle(num_selfplay_envs, num_bot_envs, map_path, max_steps, maps=None, game_maps=None, partial_obs=False):
     from oracle_py import OracleVecEnv
 
     paths = maps or [os.path.join(MAPS, map_path)]
     return OracleVecEnv(num_selfplay_envs, num_bot_envs, paths, max_steps=max_steps, ai2s=["passiveAI"] * num_bot_envs,
-                        game_maps=game_maps)
+                        game_maps=game_maps, partial_obs=partial_obs)
 
 
 def test_native_library_is_the_engine():
@@ -66,14 +66,14 @@ def test_kat_reward():
     kat.check_rewards(make_gpu_env)
 
 
-def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_tensors=False):
+def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_tensors=False, partial_obs=False):
     """Lock-step GPU vs oracle rollout; compares masks, obs, rewards, dones."""
     from oracle_py import sample_actions
 
     torch = _torch()
     g = make_gpu_env(nsp, nbot, map_path, max_steps, return_tensors=return_tensors,
-                     obs_dtype=torch.int32 if return_tensors else None)
-    o = make_oracle(nsp, nbot, map_path, max_steps)
+                     obs_dtype=torch.int32 if return_tensors else None, partial_obs=partial_obs)
+    o = make_oracle(nsp, nbot, map_path, max_steps, partial_obs=partial_obs)
     og = np.asarray(g.reset().cpu() if return_tensors else g.reset())
     oo = o.reset()
     np.testing.assert_array_equal(og, oo)
@@ -135,6 +135,21 @@ def test_masked_rollout_bit_exact(map_path, nsp, nbot, max_steps, steps):
 @pytest.mark.parametrize("map_path", ["maps/16x16/basesWorkers16x16.xml", "maps/4x4/baseTwoWorkers4x4.xml"])
 def test_adversarial_rollout_bit_exact(map_path, mode):
     _rollout(map_path, 32, 16, 300, 400, seed=5, mode=mode)
+
+
+@pytest.mark.parametrize("map_path,nsp,nbot", [
+    ("maps/16x16/basesWorkers16x16.xml", 32, 8),
+    ("maps/8x8/basesWorkers8x8.xml", 32, 8),
+    ("maps/24x24/basesWorkers24x24.xml", 8, 4),
+    ("maps/4x4/baseTwoWorkers4x4.xml", 16, 16),
+])
+def test_partial_obs_rollout_bit_exact(map_path, nsp, nbot):
+    """partial_obs=True (31 planes, PartiallyObservableGameState)."""
+    _rollout(map_path, nsp, nbot, 250, 500, seed=17, partial_obs=True)
+
+
+def test_partial_obs_tensor_path():
+    _rollout("maps/16x16/basesWorkers16x16.xml", 16, 0, 300, 200, seed=4, return_tensors=True, partial_obs=True)
 
 
 def test_tensor_path_bit_exact():

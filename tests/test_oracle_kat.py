@@ -91,3 +91,48 @@ def test_random_rollout_invariants():
             # owned units never carry a negative hp
             assert (cells[live, 2] > 0).all()
     assert dones >= 16 * 2  # max_steps=300 forces at least 3 episodes per env
+
+
+README_PO_WORKER = [0, 1, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 1, 0]
+PO_EMPTY = [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 1, 0]
+
+
+def test_partial_obs_readme_vector():
+    """README.md:90-92: a worker not visible to the opponent encodes as the
+    29-vector + [1,0]; enemy units (and resources) outside the player's sight
+    read as empty cells (PartiallyObservableGameState)."""
+    e = OracleVecEnv(2, 0, [os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml")], max_steps=100, partial_obs=True)
+    obs = e.reset()
+    assert obs.shape == (2, 16, 16, 31)
+    assert (obs.sum(-1) == 7).all()
+    assert obs[0, 1, 1].tolist() == README_PO_WORKER        # own worker (1,1), opponent 13 cells away
+    assert obs[1, 14, 14].tolist() == README_PO_WORKER      # p1's view of its own worker
+    for y, x in [(13, 13), (14, 14), (14, 15), (15, 15)]:   # p1 units + far resources hidden from p0
+        assert obs[0, y, x].tolist() == PO_EMPTY, (y, x)
+    assert obs[0, 0, 0, 13 + 1] == 1                         # resource (0,0) within the worker's sight
+    assert obs[0, 0, 0, 29] == 1                             # ... and not observable by p1
+    # full observability still sees everything
+    f = OracleVecEnv(2, 0, [os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml")], max_steps=100).reset()
+    assert f[0, 14, 14, 10 + 2] == 1
+
+
+def test_partial_obs_rollout_invariants():
+    e = OracleVecEnv(16, 0, [os.path.join(MAPS, "maps/8x8/basesWorkers8x8.xml")], max_steps=200, partial_obs=True)
+    full = OracleVecEnv(16, 0, [os.path.join(MAPS, "maps/8x8/basesWorkers8x8.xml")], max_steps=200)
+    e.reset()
+    full.reset()
+    for s in range(300):
+        m = e.get_action_mask()
+        np.testing.assert_array_equal(m, full.get_action_mask())   # masks ignore fog (own units only)
+        a = sample_actions(m, 3, s)
+        obs, r, d, _ = e.step(a)
+        fo, fr, fd, _ = full.step(a)
+        np.testing.assert_array_equal(r, fr)
+        np.testing.assert_array_equal(d, fd)
+        assert (obs.sum(-1) == 7).all()
+        # every unit the player sees is where the full observation has it
+        seen = obs[..., 13] == 0
+        np.testing.assert_array_equal(obs[..., :29][seen], fo[seen])
+        # own units are never hidden
+        own = fo[..., 11] == 1
+        np.testing.assert_array_equal(obs[..., :29][own], fo[own])
