@@ -43,6 +43,11 @@ extern "C" {
 #define MRTS_AI_LIGHT_RUSH 2
 #define MRTS_AI_RANDOM_BIASED 3
 #define MRTS_AI_COAC 4
+#define MRTS_AI_PO_WORKER_RUSH 5
+#define MRTS_AI_PO_LIGHT_RUSH 6
+#define MRTS_AI_PO_HEAVY_RUSH 7
+#define MRTS_AI_PO_RANGED_RUSH 8
+#define MRTS_AI_COUNT 9
 
 #define MRTS_OBS_INT32 0
 #define MRTS_OBS_FLOAT32 1

@@ -158,6 +158,8 @@ struct mrts_vec {
     std::vector<int32_t> bot_ai;
     // workspace carving
     size_t off_cells = 0, off_genv = 0, off_mcells = 0, off_mwall = 0, off_mscal = 0, off_scratch = 0, total = 0;
+    size_t off_botai = 0, off_aa = 0, off_botpa = 0;
+    int nbot_active = 0;
     unsigned char *ws = nullptr;
     std::vector<int32_t> scratch_host;
     std::string err, utt;
@@ -216,10 +218,18 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
         h->game_map[g] = m;
     }
     h->bot_ai.assign(h->nbot, MRTS_AI_PASSIVE);
+    h->nbot_active = 0;
     for (int j = 0; j < h->nbot; j++) {
         int a = cfg->bot_ai ? cfg->bot_ai[j] : MRTS_AI_PASSIVE;
-        if (a != MRTS_AI_PASSIVE) return fail(h, MRTS_ENOTIMPL, "only passiveAI bots run on the device so far (DESIGN.md §8)");
+        if (a < 0 || a >= MRTS_AI_COUNT) return fail(h, MRTS_EINVAL, "bot_ai: unknown MRTS_AI_* id");
         h->bot_ai[j] = a;
+        h->nbot_active += a != MRTS_AI_PASSIVE;
+    }
+    if (h->nbot_active) {
+        if (h->W > 32 || h->H > 64)
+            return fail(h, MRTS_ENOTIMPL, "device bots need maps at most 32 wide and 64 high (one bit word per row)");
+        if (mrts_engine_bot_lds_bytes(h->HW, h->W) > 65536)
+            return fail(h, MRTS_ENOTIMPL, "map too large for the bot kernel's LDS");
     }
     size_t o = 0;
     h->off_cells = o; o = align256(o + (size_t)h->ngames * h->HW * sizeof(int4));
@@ -228,6 +238,9 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     h->off_mwall = o; o = align256(o + (size_t)cfg->num_maps * h->HW);
     h->off_mscal = o; o = align256(o + (size_t)cfg->num_maps * MRTS_MAP_SCALARS * sizeof(int32_t));
     h->off_scratch = o; o = align256(o + (size_t)2 * h->ngames * sizeof(int32_t));
+    h->off_botai = o; o = align256(o + (size_t)(h->nbot + 1) * sizeof(int32_t));
+    h->off_aa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * h->HW * 2 * sizeof(int4) : 0));
+    h->off_botpa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * h->HW * sizeof(int32_t) : 0));
     h->total = o;
     h->err.clear();
     return MRTS_OK;
@@ -269,6 +282,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
         (e = hipMemcpyAsync(h->ws + h->off_mwall, mw.data(), mw.size(), hipMemcpyHostToDevice, s)) ||
         (e = hipMemcpyAsync(h->ws + h->off_mscal, ms.data(), ms.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) ||
         (e = hipMemcpyAsync(h->ws + h->off_genv, genv.data(), genv.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) ||
+        (h->nbot && (e = hipMemcpyAsync(h->ws + h->off_botai, h->bot_ai.data(), h->nbot * sizeof(int32_t), hipMemcpyHostToDevice, s))) ||
         (e = hipStreamSynchronize(s)))
         return hip_fail(h, e, "bind_workspace upload");
     EngineParams &p = h->base;
@@ -287,6 +301,10 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.max_steps = h->max_steps;
     p.obs_float = h->obs_float;
     p.partial_obs = h->partial_obs;
+    p.bot_ai = (const int32_t *)(h->ws + h->off_botai);
+    p.aa = h->nbot_active ? (int4 *)(h->ws + h->off_aa) : nullptr;
+    p.botpa = h->nbot_active ? (int32_t *)(h->ws + h->off_botpa) : nullptr;
+    p.nbot_active = h->nbot_active;
     h->err.clear();
     return MRTS_OK;
 }
@@ -320,7 +338,8 @@ int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *
     p.obs = obs;
     p.raw_reward = raw_reward;
     p.done = done;
-    hipError_t e = mrts_engine_step(&p, (hipStream_t)stream);
+    hipError_t e = mrts_engine_bots(&p, (hipStream_t)stream);
+    if (!e) e = mrts_engine_step(&p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
 }
 
@@ -345,7 +364,8 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
     p.done0 = done0;
     for (int k = 0; k < 6; k++) p.rw[k] = h->rw[k];
     p.shaping = h->shaping;
-    hipError_t e = mrts_engine_step(&p, (hipStream_t)stream);
+    hipError_t e = mrts_engine_bots(&p, (hipStream_t)stream);
+    if (!e) e = mrts_engine_step(&p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
 }
 

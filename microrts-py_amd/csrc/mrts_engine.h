@@ -26,13 +26,20 @@ struct EngineParams {
     uint8_t *done0;         // [N] or null (torch.bool storage)
     double rw[6];
     int shaping;
+    // device bots (mrts_bots.hip): bot game b = game nsp_games + b
+    const int32_t *bot_ai;  // [Gb] MRTS_AI_*
+    int4 *aa;               // [Gb][HW][2] AbstractionLayerAI.actions
+    int32_t *botpa;         // [Gb][HW] bot PlayerAction, cell | code << 16; null = none
+    int nbot_active;        // bot games whose AI is not passiveAI
 };
 
 extern "C" {
 hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t *games, const int32_t *maps, int count);
 hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
+hipError_t mrts_engine_bots(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
 size_t mrts_engine_lds_bytes(int HW, int W);
+size_t mrts_engine_bot_lds_bytes(int HW, int W);
 }
 #endif

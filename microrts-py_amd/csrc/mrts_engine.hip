@@ -23,216 +23,9 @@
 #include "mrts_engine.h"
 #include "mrts_layout.h"
 
+#include "mrts_rules.h"
+
 namespace mrts {
-
-// ---------------------------------------------------------------------------
-// rts.units.UnitTypeTable() -- VERSION_ORIGINAL (+ UnitType field defaults).
-enum { RESOURCE = 0, BASE, BARRACKS, WORKER, LIGHT, HEAVY, RANGED };
-enum { A_NONE = 0, A_MOVE, A_HARVEST, A_RETURN, A_PRODUCE, A_ATTACK };
-
-__device__ __forceinline__ int ut_cost(int t) { return t == BASE ? 10 : t == BARRACKS ? 5 : (t >= LIGHT ? 2 : 1); }
-__device__ __forceinline__ int ut_hp(int t) { return t == BASE ? 10 : (t == BARRACKS || t == LIGHT || t == HEAVY) ? 4 : 1; }
-__device__ __forceinline__ int ut_damage(int t) { return t == LIGHT ? 2 : t == HEAVY ? 4 : 1; }
-__device__ __forceinline__ int ut_range(int t) { return t == RANGED ? 3 : 1; }
-__device__ __forceinline__ int ut_produce_time(int t) {
-    return t == BASE ? 250 : t == BARRACKS ? 200 : t == WORKER ? 50 : t == LIGHT ? 80 : t == HEAVY ? 120 : t == RANGED ? 100 : 10;
-}
-__device__ __forceinline__ int ut_move_time(int t) { return t == LIGHT ? 8 : t == HEAVY ? 12 : 10; }
-__device__ __forceinline__ int ut_attack_time(int t) { return t >= WORKER ? 5 : 10; }
-__device__ __forceinline__ int ut_harvest_time(int t) { return t == WORKER ? 20 : 10; }
-__device__ __forceinline__ int ut_return_time(int) { return 10; }
-__device__ __forceinline__ int ut_harvest_amount(int) { return 1; }
-__device__ __forceinline__ int ut_sight(int t) {
-    return t == BASE ? 5 : (t == BARRACKS || t == WORKER || t == RANGED) ? 3 : (t == LIGHT || t == HEAVY) ? 2 : 0;
-}
-__device__ __forceinline__ bool ut_can_move(int t) { return t >= WORKER; }
-__device__ __forceinline__ bool ut_can_attack(int t) { return t >= WORKER; }
-__device__ __forceinline__ bool ut_can_harvest(int t) { return t == WORKER; }
-__device__ __forceinline__ bool ut_is_stockpile(int t) { return t == BASE; }
-// bitmask of produced unit types
-__device__ __forceinline__ int ut_produces(int t) {
-    return t == BASE ? (1 << WORKER) : t == BARRACKS ? ((1 << LIGHT) | (1 << HEAVY) | (1 << RANGED)) : t == WORKER ? ((1 << BASE) | (1 << BARRACKS)) : 0;
-}
-
-// ---------------------------------------------------------------------------
-// Packed words (mrts_layout.h)
-__device__ __forceinline__ int u_type(uint32_t w) { return (int)(w & 15u) - 1; }
-__device__ __forceinline__ int u_owner(uint32_t w) { return (int)((w >> 4) & 3u) - 1; }
-__device__ __forceinline__ int u_hp(uint32_t w) { return (int)((w >> 6) & 1023u); }
-__device__ __forceinline__ int u_res(uint32_t w) { return (int)(w >> 16); }
-__device__ __forceinline__ uint32_t u_make(int type, int owner, int hp, int res) {
-    return (uint32_t)(type + 1) | ((uint32_t)(owner + 1) << 4) | ((uint32_t)hp << 6) | ((uint32_t)res << 16);
-}
-__device__ __forceinline__ uint32_t u_with_hp(uint32_t w, int hp) { return (w & ~(1023u << 6)) | ((uint32_t)hp << 6); }
-__device__ __forceinline__ uint32_t u_with_res(uint32_t w, int res) { return (w & 0xFFFFu) | ((uint32_t)res << 16); }
-
-// action code (12 bits): type | param << 3 | utype << 9 ; action word = code + 1 | (done + 1) << 12
-__device__ __forceinline__ int code_make(int type, int param, int utype) { return type | (param << 3) | (utype << 9); }
-__device__ __forceinline__ int code_type(int code) { return code & 7; }
-__device__ __forceinline__ int code_param(int code) { return (code >> 3) & 63; }
-__device__ __forceinline__ int code_utype(int code) { return (code >> 9) & 7; }
-__device__ __forceinline__ uint32_t act_make(int code, int done) { return (uint32_t)(code + 1) | ((uint32_t)(done + 1) << 12); }
-__device__ __forceinline__ int act_code(uint32_t a) { return (int)(a & 0xFFFu) - 1; }
-__device__ __forceinline__ int act_done(uint32_t a) { return (int)(a >> 12) - 1; }
-__device__ __forceinline__ uint32_t seq_make(int time, int player, int rank) {
-    return ((uint32_t)time << 13) | ((uint32_t)player << 12) | (uint32_t)rank;
-}
-__device__ __forceinline__ int seq_time(uint32_t s) { return (int)(s >> 13); }
-
-// UnitAction.ETA for a non-NONE code executed by a unit of type t
-__device__ __forceinline__ int eta_code(int code, int t) {
-    switch (code_type(code)) {
-    case A_MOVE: return ut_move_time(t);
-    case A_HARVEST: return ut_harvest_time(t);
-    case A_RETURN: return ut_return_time(t);
-    case A_PRODUCE: return ut_produce_time(code_utype(code));
-    case A_ATTACK: return ut_attack_time(t);
-    }
-    return 0;
-}
-
-__device__ __forceinline__ int dir_dx(int d) { return d == 1 ? 1 : d == 3 ? -1 : 0; }
-__device__ __forceinline__ int dir_dy(int d) { return d == 2 ? 1 : d == 0 ? -1 : 0; }
-
-struct Grid {
-    int W, H, HW;
-};
-
-// neighbour cell in direction d, or -1 when off the map
-__device__ __forceinline__ int nb_cell(const Grid& gd, int c, int d) {
-    int x = c % gd.W + dir_dx(d), y = c / gd.W + dir_dy(d);
-    return (x < 0 || y < 0 || x >= gd.W || y >= gd.H) ? -1 : y * gd.W + x;
-}
-
-// Unit.getUnitActions membership test (UnitAction.equals), i.e.
-// Unit.canExecuteAction for a decoded action code of the unit at cell c.
-__device__ bool legal_code(const Grid& gd, int c, int code, const uint32_t* s_unit, const uint8_t* s_wall, int res_player) {
-    uint32_t u = s_unit[c];
-    int t = u_type(u), owner = u_owner(u);
-    int type = code_type(code), param = code_param(code);
-    switch (type) {
-    case A_NONE: return true;
-    case A_MOVE: {
-        if (!ut_can_move(t)) return false;
-        int n = nb_cell(gd, c, param);
-        return n >= 0 && !s_wall[n] && s_unit[n] == 0;
-    }
-    case A_HARVEST: {
-        if (!ut_can_harvest(t) || u_res(u) != 0) return false;
-        int n = nb_cell(gd, c, param);
-        return n >= 0 && s_unit[n] != 0 && u_type(s_unit[n]) == RESOURCE;
-    }
-    case A_RETURN: {
-        if (!ut_can_harvest(t) || u_res(u) <= 0) return false;
-        int n = nb_cell(gd, c, param);
-        return n >= 0 && s_unit[n] != 0 && ut_is_stockpile(u_type(s_unit[n])) && u_owner(s_unit[n]) == owner;
-    }
-    case A_PRODUCE: {
-        int ut = code_utype(code);
-        if (!((ut_produces(t) >> ut) & 1) || res_player < ut_cost(ut)) return false;
-        int n = nb_cell(gd, c, param);
-        return n >= 0 && !s_wall[n] && s_unit[n] == 0;
-    }
-    case A_ATTACK: {
-        if (!ut_can_attack(t)) return false;
-        int dx = param % MRTS_ATTACK_GRID - MRTS_ATTACK_GRID / 2, dy = param / MRTS_ATTACK_GRID - MRTS_ATTACK_GRID / 2;
-        int r = ut_range(t);
-        if (dx * dx + dy * dy > r * r) return false;
-        int x = c % gd.W + dx, y = c / gd.W + dy;
-        if (x < 0 || y < 0 || x >= gd.W || y >= gd.H) return false;
-        uint32_t o = s_unit[y * gd.W + x];
-        int oo = u_owner(o);
-        return o != 0 && oo >= 0 && oo != owner;
-    }
-    }
-    return false;
-}
-
-// UnitAction.getValidActionArray for the idle unit at c: 79 bits (bit 0 = source)
-__device__ void cell_mask(const Grid& gd, int c, int player, const uint32_t* s_unit, const uint32_t* s_act,
-                          const uint8_t* s_wall, int res_player, uint32_t m[3]) {
-    m[0] = m[1] = m[2] = 0;
-    uint32_t u = s_unit[c];
-    if (u == 0 || u_owner(u) != player || s_act[c] != 0) return;
-    auto setb = [&](int b) { m[b >> 5] |= 1u << (b & 31); };
-    const int T = 1, MV = 7, HV = 11, RT = 15, PD = 19, PT = 23, AT = 30;
-    setb(0);
-    setb(T + A_NONE);
-    int t = u_type(u), x = c % gd.W, y = c / gd.W;
-    int nb[4];
-    bool freec[4];
-    for (int d = 0; d < 4; d++) {
-        nb[d] = nb_cell(gd, c, d);
-        freec[d] = nb[d] >= 0 && !s_wall[nb[d]] && s_unit[nb[d]] == 0;
-    }
-    const int cc = MRTS_ATTACK_GRID / 2;
-    if (ut_can_attack(t)) {
-        int r = ut_range(t);
-        for (int dy = -r; dy <= r; dy++)
-            for (int dx = -r; dx <= r; dx++) {
-                if (dx * dx + dy * dy > r * r) continue;
-                int xx = x + dx, yy = y + dy;
-                if (xx < 0 || yy < 0 || xx >= gd.W || yy >= gd.H) continue;
-                uint32_t o = s_unit[yy * gd.W + xx];
-                int oo = u_owner(o);
-                if (o != 0 && oo >= 0 && oo != player) {
-                    setb(T + A_ATTACK);
-                    setb(AT + (cc + dy) * MRTS_ATTACK_GRID + (cc + dx));
-                }
-            }
-    }
-    if (ut_can_harvest(t)) {
-        int ur = u_res(u);
-        for (int d = 0; d < 4; d++) {
-            if (nb[d] < 0 || s_unit[nb[d]] == 0) continue;
-            uint32_t o = s_unit[nb[d]];
-            if (ur == 0 && u_type(o) == RESOURCE) {
-                setb(T + A_HARVEST);
-                setb(HV + d);
-            }
-            if (ur > 0 && ut_is_stockpile(u_type(o)) && u_owner(o) == player) {
-                setb(T + A_RETURN);
-                setb(RT + d);
-            }
-        }
-    }
-    int prod = ut_produces(t);
-    bool anyfree = freec[0] || freec[1] || freec[2] || freec[3];
-    if (prod && anyfree) {
-        for (int ut = 0; ut < MRTS_NTYPES; ut++) {
-            if (!((prod >> ut) & 1) || res_player < ut_cost(ut)) continue;
-            setb(T + A_PRODUCE);
-            setb(PT + ut);
-            for (int d = 0; d < 4; d++)
-                if (freec[d]) setb(PD + d);
-        }
-    }
-    if (ut_can_move(t) && anyfree) {
-        setb(T + A_MOVE);
-        for (int d = 0; d < 4; d++)
-            if (freec[d]) setb(MV + d);
-    }
-}
-
-// one-hot word of vec_env.py:311-321 for the cell (perspective `player`).
-// Partial observability (P == 31, PartiallyObservableGameState): `shown` is 0
-// for a unit the player cannot see (the cell reads as empty); bits 29/30 are
-// the visibility plane: the shown unit is visible to the opponent.
-__device__ __forceinline__ uint32_t cell_onehot(uint32_t u, uint32_t a, uint8_t wall, int player, int P = 29,
-                                                bool shown = true, bool opp_sees = false) {
-    uint32_t b = 0;
-    if (!shown) u = 0;
-    if (P == 31) b |= 1u << (29 + ((u != 0 && opp_sees) ? 1 : 0));
-    if (u == 0) {
-        b |= 1u | (1u << 5) | (1u << 10) | (1u << 13) | (1u << 21);
-    } else {
-        int hp = min(max(u_hp(u), 0), 4), res = min(u_res(u), 4), ow = u_owner(u);
-        int rel = ow < 0 ? 0 : (ow == player ? 1 : 2);
-        int at = a ? min(code_type(act_code(a)), 5) : 0;
-        b |= (1u << hp) | (1u << (5 + res)) | (1u << (10 + rel)) | (1u << (13 + u_type(u) + 1)) | (1u << (21 + at));
-    }
-    return b | (1u << (27 + (wall ? 1 : 0)));
-}
 
 // ---------------------------------------------------------------------------
 // LDS carving (all dynamic, 16-byte aligned pieces: cdna_hip_programming §6 G17)
@@ -245,6 +38,7 @@ struct Lds {
     int32_t* resv;   // reservation holder per cell
     int32_t* list;   // compact cell lists
     int32_t* prod;   // pending produce cells
+    int32_t* blist;  // the bot's PlayerAction order (bot games)
     int4* snap;      // ready-action snapshots
     uint32_t* mbits; // mask bits, 3 words per cell (mask kernel)
     uint8_t* wall;
@@ -253,8 +47,11 @@ struct Lds {
     uint32_t* vis;   // [2][HW/32+1] cells observable by player 0 / 1 (partial obs)
     int* sc;         // scalars
 };
-enum { SC_TIME = 0, SC_RES0, SC_RES1, SC_UID, SC_STEPS, SC_MAP, SC_ERR, SC_NPROD, SC_CNT, SC_GO, SC_WIN,
-       SC_R0 = 16, /* rewards: [player][6] as ints */ SC_WORDS = 32 };
+// L.sc[0 .. MRTS_GENV_WORDS) mirrors genv (load_game / store_game)
+enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_UID = MRTS_G_NEXT_UID,
+       SC_STEPS = MRTS_G_STEPS, SC_MAP = MRTS_G_MAP, SC_ERR = MRTS_G_ERR, SC_AA_N = MRTS_G_AA_N, SC_TICKS = MRTS_G_TICKS,
+       SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_WORDS = 32 };
+static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -283,7 +80,7 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     L.resv = (int32_t*)take(4 * (size_t)HW);
     L.list = (int32_t*)take(4 * (size_t)HW);
     L.prod = (int32_t*)take(4 * (size_t)HW);
-    take(4 * (size_t)HW);
+    L.blist = (int32_t*)take(4 * (size_t)HW);
     L.snap = (int4*)take(16 * (size_t)HW);
     L.mbits = (uint32_t*)take(12 * (size_t)HW);
     L.wall = (uint8_t*)take((size_t)HW);
@@ -461,7 +258,7 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
     Lds L = carve(smem, p.HW, p.W, NT);
     int g = games ? games[blockIdx.x] : blockIdx.x;
     int map = maps ? maps[blockIdx.x] : p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
-    if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
+    if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = threadIdx.x == SC_TICKS ? p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_TICKS] : 0;
     __syncthreads();
     reset_into_lds<NT>(p, L, map);
     __syncthreads();
@@ -526,15 +323,20 @@ enum : uint32_t { CAND = 1u << 31, LEGAL = 1u << 30 };
 __device__ __forceinline__ int res_of(const Lds& L, int player) { return L.sc[SC_RES0 + player]; }
 
 // PlayerAction.fromVectorAction consistency filter + GameState.issueSafe/issue
-// for one player's rows (lane 0 only).  Rows are L.list[0..n) ascending.
-__device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd, int q, int n) {
+// for one player's PlayerAction (lane 0 only).  Entries are list[0..n) in
+// PlayerAction order with their codes in L.aux: the agent's rows (ascending
+// cells, `vector` = true: the fromVectorAction consistency filter applies and
+// the LinkedHashMap rank is the cell) or a device bot's PlayerAction (already
+// consistent, rank = position in the list).
+__device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd, int q, const int32_t* list, int n,
+                             bool vector) {
     const int time = L.sc[SC_TIME];
     // --- fromVectorAction: ResourceUsage.consistentWith(pa.ru) ----------------
     const int nposw = (gd.HW + 2 * gd.W + 31) / 32;
     for (int i = 0; i < nposw; i++) L.posbits[i] = 0;
     int pa_cost = 0;
-    for (int i = 0; i < n; i++) {
-        int c = L.list[i];
+    for (int i = 0; vector && i < n; i++) {
+        int c = list[i];
         uint32_t nw = L.aux[c];
         if (u_owner(L.unit[c]) != q) continue;
         int code = (int)(nw & 0xFFFu), type = code_type(code);
@@ -555,14 +357,14 @@ __device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd
     // --- issueSafe + issue -----------------------------------------------------
     int* rw = L.sc + SC_R0 + 6 * q;
     for (int i = 0; i < n; i++) {
-        int c = L.list[i];
+        int c = list[i];
         uint32_t nw = L.aux[c];
         if (u_owner(L.unit[c]) != q || !(nw & CAND)) continue;
         const int ut = u_type(L.unit[c]);
         int code = (int)(nw & 0xFFFu);
         // issueSafe: illegal -> NONE with the same ETA
-        int cur = code, cur_dur = 1;   // cur_dur: duration when cur is NONE
-        if (code_type(code) == A_NONE) cur_dur = 1;
+        int cur = code, cur_dur = 1;   // cur_dur: duration when cur is NONE (a NONE code's param)
+        if (code_type(code) == A_NONE) cur_dur = code_param(code);
         else if (!(nw & LEGAL)) { cur_dur = eta_code(code, ut); cur = A_NONE; }
         int te = cur;                  // the action the TraceEntry records
         const int ctype = code_type(cur);
@@ -622,7 +424,7 @@ __device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd
         const int ft = code_type(cur);
         const int done = ft == A_NONE ? time + cur_dur : time + eta_code(cur, ut);
         L.act[c] = act_make(cur, done);
-        L.seq[c] = seq_make(time, q, c);
+        L.seq[c] = seq_make(time, q, vector ? c : i);
         if (ft == A_MOVE || ft == A_PRODUCE) {
             L.resv[nb_cell(gd, c, code_param(cur))] = c;
             if (ft == A_PRODUCE) L.prod[L.sc[SC_NPROD]++] = c;
@@ -750,7 +552,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
                     const int64_t* r = p.actions + row * 7;
                     int64_t ty = r[0];
                     int code = -1;
-                    if (ty == A_NONE) code = code_make(A_NONE, 0, 0);
+                    if (ty == A_NONE) code = code_make(A_NONE, 1, 0);   // NONE(1): param = duration
                     else if (ty >= A_MOVE && ty <= A_RETURN) {
                         int64_t d = r[ty];
                         if (d >= 0 && d < 4) code = code_make((int)ty, (int)d, 0);
@@ -769,6 +571,16 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             }
         }
         L.aux[c] = nw;
+    }
+    __syncthreads();
+    // the device bot's PlayerAction for player 1 (k_bot, computed on the state
+    // before this tick's issues: JNIGridnetClient.gameStep order)
+    const int npa = (!G.selfplay && p.botpa) ? L.sc[SC_NPA] : 0;
+    for (int i = threadIdx.x; i < npa; i += NT) {
+        const int e = p.botpa[(size_t)(g - p.nsp_games) * HW + i];
+        const int c = e & 0xFFFF, code = e >> 16;
+        L.blist[i] = c;
+        L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, 1)) ? LEGAL : 0u) | (uint32_t)code;
     }
     __syncthreads();
     // pending move/produce reservations (ResourceUsage of unitActions)
@@ -790,8 +602,9 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // (2) ordered part: p0 then p1 (bot envs: the passive bot issues only NONEs)
     if (threadIdx.x == 0) {
         L.sc[SC_NPROD] = nprod;
-        issue_player(p, L, gd, 0, nrows);
-        if (G.selfplay) issue_player(p, L, gd, 1, nrows);
+        issue_player(p, L, gd, 0, L.list, nrows, true);
+        if (G.selfplay) issue_player(p, L, gd, 1, L.list, nrows, true);
+        else if (npa > 0) issue_player(p, L, gd, 1, L.blist, npa, false);
     }
     __syncthreads();
     // (3) fillWithNones(gs, player, 1) for every idle unit (both players)
@@ -815,6 +628,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     }, L.list, L.ballot);
     if (threadIdx.x == 0) {
         L.sc[SC_TIME] = now;
+        L.sc[SC_TICKS]++;
         if (now >= MRTS_MAX_TIME) L.sc[SC_ERR] |= MRTS_ERR_TIME_OVERFLOW;
         if (nready > 0) {
             for (int i = 0; i < nready; i++) {
@@ -873,6 +687,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     __syncthreads();
     if (reset) {
         reset_into_lds<NT>(p, L, L.sc[SC_MAP]);
+        if (threadIdx.x == 0) L.sc[SC_AA_N] = 0;   // ai2.reset()
         __syncthreads();
     } else if (threadIdx.x == 0) {
         L.sc[SC_STEPS] = steps;
@@ -918,9 +733,20 @@ __global__ __launch_bounds__(SR) void k_sample(const int32_t* __restrict__ mask,
     const int32_t* mb = mask + row0 * MRTS_MASK_CH;   // 16-B aligned: SR*312 B per block
     const int nel = rb * MRTS_MASK_CH, nv = nel >> 2;
     const int4* m4 = reinterpret_cast<const int4*>(mb);
-    for (int k = threadIdx.x; k < nv; k += SR) {
-        int4 v = m4[k];
-        if ((v.x | v.y | v.z | v.w) == 0) continue;   // most cells hold no idle unit
+    // issue every load of the block's mask rows before consuming any (the LDS
+    // atomics below would otherwise serialise one HBM round trip per load)
+    constexpr int NV = (SR * MRTS_MASK_CH / 4 + SR - 1) / SR;
+    int4 vbuf[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        const int k = j * SR + threadIdx.x;
+        vbuf[j] = k < nv ? m4[k] : make_int4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        const int k = j * SR + threadIdx.x;
+        const int4 v = vbuf[j];
+        if (k >= nv || (v.x | v.y | v.z | v.w) == 0) continue;   // most cells hold no idle unit
         int e = 4 * k;
         int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
         int vv[4] = {v.x, v.y, v.z, v.w};

@@ -36,6 +36,7 @@ static const OType UT[NTYPES] = {
     /* Heavy    */ {2, 4, 4, 4, 1, 120, 12, 5, 10, 10, 1, 2, 0, 0, 0, 1, 1, 0, {0}},
     /* Ranged   */ {2, 1, 1, 1, 3, 100, 10, 5, 10, 10, 1, 3, 0, 0, 0, 1, 1, 0, {0}},
 };
+#define MAX_HW_ORACLE 4096
 #define MAX_ATTACK_RANGE 3 /* UnitTypeTable.getMaxAttackRange(); 7x7 grid at vec_env.py:234 */
 #define ATTACK_GRID 7
 
@@ -104,6 +105,8 @@ struct OVec {
     int *bot_ai;
     OGS *gs;
     int *env_steps; /* per game (selfplay pairs step together)                */
+    uint32_t *ticks;/* per game: steps since creation (bot RNG counter)        */
+    struct OAAMapS *aam; /* per game: the bot's AbstractionLayerAI.actions     */
     int32_t *raw;   /* [N][P_raw][H][W] last response observation             */
 };
 
@@ -292,12 +295,18 @@ static void gs_load(OGS *g, const OMap *m) { /* PhysicalGameState.load + new Gam
 
 /* ---- Unit.getUnitActions(gs, noneDuration) ------------------------------ */
 #define MAXLIST 64
-static int unit_actions(const OGS *g, int ui, int none_duration, OAct *l) {
+/* getUnitAt in a game state some of whose units are hidden (a bot's
+ * PartiallyObservableGameState); hidden == NULL is the full state. */
+static int unit_at_h(const OGS *g, const uint8_t *hidden, int x, int y) {
+    int i = unit_at(g, x, y);
+    return (i >= 0 && hidden && hidden[i]) ? -1 : i;
+}
+static int unit_actions_h(const OGS *g, const uint8_t *hidden, int ui, int none_duration, OAct *l) {
     const OUnit *u = &g->u[ui];
     const OType *t = &UT[u->type];
     int n = 0, x = u->x, y = u->y;
-    int uup = unit_at(g, x, y - 1), uright = unit_at(g, x + 1, y), udown = unit_at(g, x, y + 1),
-        uleft = unit_at(g, x - 1, y);
+    int uup = unit_at_h(g, hidden, x, y - 1), uright = unit_at_h(g, hidden, x + 1, y),
+        udown = unit_at_h(g, hidden, x, y + 1), uleft = unit_at_h(g, hidden, x - 1, y);
     if (t->can_attack) {
         if (t->range == 1) {
             int nb[4] = {uup, uright, udown, uleft};
@@ -312,7 +321,7 @@ static int unit_actions(const OGS *g, int ui, int none_duration, OAct *l) {
             int sq = t->range * t->range;
             for (int i = 0; i < g->nu; i++) {
                 const OUnit *o = &g->u[i];
-                if (!o->alive || o->player < 0 || o->player == u->player) continue;
+                if (!o->alive || (hidden && hidden[i]) || o->player < 0 || o->player == u->player) continue;
                 int dx = o->x - x, dy = o->y - y;
                 if (dx * dx + dy * dy <= sq) {
                     OAct a = {A_ATTACK, DIRECTION_NONE, o->x, o->y, -1};
@@ -363,6 +372,9 @@ static int unit_actions(const OGS *g, int ui, int none_duration, OAct *l) {
     }
     l[n++] = act_none(none_duration);
     return n;
+}
+static int unit_actions(const OGS *g, int ui, int none_duration, OAct *l) {
+    return unit_actions_h(g, NULL, ui, none_duration, l);
 }
 
 static int can_execute(const OGS *g, int ui, const OAct *a) { /* Unit.canExecuteAction */
@@ -720,6 +732,8 @@ static void unit_masks(const OGS *g, int player, int32_t *m) {
     }
 }
 
+#include "mrts_oracle_ai.c"
+
 /* ------------------------------------------------------------------------- */
 OVec *ovec_create(int num_selfplay, int num_bot, int max_steps, int partial_obs, const OMap *maps,
                   int num_maps, const int32_t *game_map, const int32_t *bot_ai) {
@@ -750,6 +764,8 @@ OVec *ovec_create(int num_selfplay, int num_bot, int max_steps, int partial_obs,
     for (int i = 0; i < num_bot; i++) v->bot_ai[i] = bot_ai ? bot_ai[i] : OAI_PASSIVE;
     v->gs = (OGS *)calloc(v->ngames, sizeof(OGS));
     v->env_steps = (int *)calloc(v->ngames, sizeof(int));
+    v->ticks = (uint32_t *)calloc(v->ngames, sizeof(uint32_t));
+    v->aam = (OAAMap *)calloc(v->ngames, sizeof(OAAMap));
     v->raw = (int32_t *)calloc((size_t)v->nenvs * (partial_obs ? 7 : 6) * v->W * v->H, sizeof(int32_t));
     return v;
 }
@@ -770,6 +786,9 @@ void ovec_destroy(OVec *v) {
     free(v->bot_ai);
     free(v->gs);
     free(v->env_steps);
+    free(v->ticks);
+    for (int i = 0; i < v->ngames; i++) free(v->aam[i].e);
+    free(v->aam);
     free(v->raw);
     free(v);
 }
@@ -800,6 +819,7 @@ void ovec_reset_game(OVec *v, int game, int map_id) {
     v->game_map[game] = map_id;
     gs_load(&v->gs[game], &v->maps[map_id]);
     v->env_steps[game] = 0;
+    v->aam[game].n = 0; /* ai2.reset() */
     game_obs(v, game);
 }
 
@@ -833,7 +853,7 @@ void ovec_step(OVec *v, const int64_t *actions, const int32_t *src, double *rewa
             issue_safe(g, &pa1);
         } else { /* JNIGridnetClient.gameStep: both actions, then issue */
             jni_get_action(g, 0, actions + (size_t)e0 * HW * 7, src + (size_t)e0 * HW, &pa0);
-            passive_get_action(g, 1, &pa1); /* device bots beyond passive: DESIGN.md §8 */
+            bot_get_action(g, v->bot_ai[gi - v->nsp / 2], v->partial_obs, gi, v->ticks[gi], &v->aam[gi], &pa1);
             issue_safe(g, &pa0);
             issue_safe(g, &pa1);
         }
@@ -845,11 +865,13 @@ void ovec_step(OVec *v, const int64_t *actions, const int32_t *src, double *rewa
         pa_free(&pa0);
         pa_free(&pa1);
         v->env_steps[gi]++;
+        v->ticks[gi]++;
         /* JNIGridnetVecClient.gameStep: done[0] || envSteps >= maxSteps -> reset,
          * keep the terminal reward/done and force done[0] = true.            */
         if (gameover || v->env_steps[gi] >= v->max_steps) {
             gs_load(g, &v->maps[v->game_map[gi]]);
             v->env_steps[gi] = 0;
+            v->aam[gi].n = 0;
             for (int k = 0; k < nv; k++) done[6 * (e0 + k)] = 1;
         }
         game_obs(v, gi);

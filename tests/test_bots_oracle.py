@@ -1,0 +1,90 @@
+"""The oracle's restated opponents (oracle/mrts_oracle_ai.c): behaviour-level
+checks on the CPU.  Bot decisions are PARITY UNPINNED against Java (the
+submodule / Coac.jar are absent); these tests pin the
+restatement's qualitative behaviour and determinism.  GPU == oracle for every
+bot is tests/test_gpu_bots.py."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MAPS
+from oracle_py import OracleVecEnv, sample_actions
+
+M16 = os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml")
+BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "POWorkerRush", "POLightRush", "POHeavyRush",
+        "PORangedRush"]
+
+
+def rollout(ai, n, steps, partial_obs=False, seed=5, noop=False, map_path=M16, max_steps=2000):
+    e = OracleVecEnv(0, n, [map_path], max_steps=max_steps, ai2s=[ai] * n, partial_obs=partial_obs)
+    e.reset()
+    out = {"loss": 0, "win": 0, "draw": 0, "obs": [], "raw": []}
+    for s in range(steps):
+        m = e.get_action_mask()
+        a = np.zeros((n, m.shape[1], 7), np.int64) if noop else sample_actions(m, seed, s)
+        o, r, d, info = e.step(a)
+        raw = np.array([i["raw_rewards"] for i in info])
+        for k in np.nonzero(d)[0]:
+            out[{-1: "loss", 0: "draw", 1: "win"}[int(raw[k, 0])]] += 1
+        out["obs"].append(o)
+        out["raw"].append(raw)
+        assert (o.sum(-1) == (7 if partial_obs else 6)).all()
+    e.close()
+    return out
+
+
+@pytest.mark.parametrize("ai", ["workerRushAI", "lightRushAI", "coacAI", "POLightRush", "PORangedRush"])
+def test_rush_bots_beat_random_agent(ai):
+    r = rollout(ai, 8, 1500)
+    assert r["loss"] >= 4 and r["win"] == 0, (r["loss"], r["win"], r["draw"])
+
+
+@pytest.mark.parametrize("ai", BOTS)
+def test_bots_are_deterministic(ai):
+    a = rollout(ai, 4, 150, partial_obs=True, seed=3)
+    b = rollout(ai, 4, 150, partial_obs=True, seed=3)
+    np.testing.assert_array_equal(np.array(a["obs"]), np.array(b["obs"]))
+    np.testing.assert_array_equal(np.array(a["raw"]), np.array(b["raw"]))
+
+
+def _enemy_types(obs):
+    """unit-type histogram of the opponent (owner plane 2) in the agent's view"""
+    enemy = obs[..., 12] == 1
+    t = np.argmax(obs[..., 13:21], -1) - 1
+    return {k: int(((t == k) & enemy).sum()) for k in range(7)}
+
+
+def test_light_rush_builds_barracks_and_lights():
+    """LightRush vs a passive agent: a barracks appears, then light units."""
+    r = rollout("lightRushAI", 2, 700, noop=True)
+    seen_barracks = any(_enemy_types(o)[2] > 0 for o in r["obs"])
+    seen_light = any(_enemy_types(o)[4] > 0 for o in r["obs"])
+    assert seen_barracks and seen_light
+
+
+def test_coac_builds_economy_and_barracks():
+    r = rollout("coacAI", 2, 800, noop=True)
+    assert any(_enemy_types(o)[2] > 0 for o in r["obs"])      # a barracks
+    assert max(_enemy_types(o)[3] for o in r["obs"]) >= 6      # 2 harvesters + defenders per base
+
+
+def test_worker_rush_trains_workers_and_wins_vs_passive():
+    r = rollout("workerRushAI", 2, 900, noop=True)
+    assert max(_enemy_types(o)[3] for o in r["obs"]) >= 3
+    assert r["loss"] >= 1
+
+
+def test_po_bots_explore_under_fog():
+    """Without partial observability the PO* rushes act as the plain rushes; under
+    fog the plain rushes never find the agent, the PO* variants do."""
+    plain = rollout("lightRushAI", 16, 2000, partial_obs=True)
+    po = rollout("POLightRush", 16, 2000, partial_obs=True)
+    assert po["loss"] > plain["loss"], (po["loss"], plain["loss"])
+
+
+def test_random_biased_acts():
+    r = rollout("randomBiasedAI", 4, 300, noop=True)
+    # the bot's units do something: action planes other than NONE appear for enemy units
+    acting = sum(int(((o[..., 12] == 1) & (o[..., 21] == 0)).sum()) for o in r["obs"])
+    assert acting > 0

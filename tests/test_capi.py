@@ -62,7 +62,6 @@ def test_create_and_info():
     (dict(num_selfplay_envs=3), "MicroRTSError"),
     (dict(max_steps=0), "MicroRTSError"),
     (dict(map_paths=["/nonexistent.xml"]), "MicroRTSError"),
-    (dict(bot_ai=[4, 0]), "MicroRTSNotImplemented"),
     (dict(bot_ai=[99, 0]), "MicroRTSError"),
 ])
 def test_create_rejects_bad_config(kw, err):

@@ -1,0 +1,83 @@
+"""Device bots (mrts_bots.hip) == the oracle's restated bots
+(oracle/mrts_oracle_ai.c), bit for bit, in lock-step rollouts through the
+product path (MicroRTSGridModeVecEnv -> libmicrorts_amd.so).  Bot behaviour vs
+Java is PARITY UNPINNED; these tests pin GPU == oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MAPS
+
+pytestmark = pytest.mark.gpu
+
+BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "POWorkerRush", "POLightRush", "POHeavyRush",
+        "PORangedRush"]
+
+
+def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=2000, mode="masked", return_tensors=False):
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv, sample_actions
+
+    w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=len(ais), max_steps=max_steps,
+                               ai2s=[getattr(microrts_ai, a) for a in ais], map_paths=[map_path], reward_weight=w,
+                               partial_obs=partial_obs, return_tensors=return_tensors,
+                               obs_dtype=torch.int32 if return_tensors else None)
+    o = OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais,
+                     partial_obs=partial_obs, reward_weight=w)
+    cpu = (lambda t: t.cpu().numpy()) if return_tensors else np.asarray
+    np.testing.assert_array_equal(cpu(g.reset()), o.reset())
+    rng = np.random.default_rng(seed)
+    n, hw = g.num_envs, g.height * g.width
+    nvec = np.array([6, 4, 4, 4, 4, 7, 49])
+    outcomes = np.zeros(3, int)
+    for s in range(steps):
+        mo = o.get_action_mask()
+        np.testing.assert_array_equal(cpu(g.get_action_mask()), mo, err_msg=f"mask step {s}")
+        a = sample_actions(mo, seed, s)
+        if mode == "mixed":
+            u = (rng.random((n, hw, 7)) * nvec).astype(np.int64)
+            a = np.where(rng.random((n, hw, 1)) < 0.3, u, a)
+        ga = torch.from_numpy(a).to(g.device) if return_tensors else a
+        og, rg, dg, ig = g.step(ga)
+        oo, ro, do, io = o.step(a)
+        np.testing.assert_array_equal(cpu(og), oo, err_msg=f"obs step {s}")
+        raw_g = np.array([i["raw_rewards"] for i in ig])
+        raw_o = np.array([i["raw_rewards"] for i in io])
+        np.testing.assert_array_equal(raw_g, raw_o, err_msg=f"raw rewards step {s}")
+        np.testing.assert_array_equal(cpu(dg), do, err_msg=f"done step {s}")
+        for k in np.nonzero(do)[0]:
+            outcomes[int(raw_o[k, 0]) + 1] += 1
+    assert g.error_flags() == 0
+    g.close()
+    o.close()
+    return outcomes
+
+
+@pytest.mark.parametrize("partial_obs", [False, True])
+@pytest.mark.parametrize("ai", BOTS)
+def test_bot_lockstep_16x16(ai, partial_obs):
+    out = lockstep([ai] * 24, "maps/16x16/basesWorkers16x16.xml", 4, 700, partial_obs=partial_obs)
+    if ai != "randomBiasedAI" and not partial_obs:
+        assert out[0] > 0   # the bot wins some games against the random agent
+
+
+@pytest.mark.parametrize("map_path", ["maps/8x8/basesWorkers8x8.xml", "maps/10x10/basesTwoWorkers10x10.xml",
+                                      "maps/24x24/basesWorkers24x24.xml", "maps/barricades24x24.xml",
+                                      "maps/4x4/baseTwoWorkers4x4.xml"])
+def test_mixed_bots_lockstep_other_maps(map_path):
+    ais = (BOTS * 3)[:16] + ["passiveAI"] * 2
+    lockstep(ais, map_path, 4, 500, max_steps=300)
+
+
+def test_bots_adversarial_agent_actions():
+    """unmasked agent actions (illegal / conflicting) against every bot"""
+    lockstep(BOTS * 2, "maps/16x16/basesWorkers16x16.xml", 2, 500, mode="mixed", max_steps=400)
+
+
+def test_bots_tensor_path_and_long_episodes():
+    lockstep(BOTS * 2, "maps/16x16/basesWorkers16x16.xml", 0, 2100, return_tensors=True, partial_obs=True)
