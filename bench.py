@@ -42,7 +42,38 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
+    ap.add_argument("--workload", default="selfplay", choices=sorted(WORKLOADS),
+                    help="selfplay = the BASELINE metric; the others are the secondary BASELINE.json configs")
     return ap.parse_args()
+
+
+# BASELINE.json configs as bench workloads: (map, selfplay envs, bot envs, bot, partial_obs).
+# The headline metric is "selfplay" (8192 envs / GPU of 16x16 basesWorkers).
+WORKLOADS = {
+    "selfplay": (MAP, "all", 0, None, False),
+    "coac": (MAP, 0, "all", "coacAI", False),          # configs[1]: envs vs device-side coacAI
+    "workerrush": (MAP, 0, "all", "workerRushAI", False),
+    "partial_obs": (MAP, "all", 0, None, True),       # configs[3]: partial_obs=True, 31 planes
+    "8x8": ("maps/8x8/basesWorkers8x8.xml", "all", 0, None, False),
+    "24x24": ("maps/24x24/basesWorkers24x24.xml", "all", 0, None, False),
+}
+
+
+WORKLOAD_DESC = {
+    "selfplay": "16x16 basesWorkers selfplay, random masked actions (device Philox sampler), get_action_mask+sample+step per env-step",
+    "coac": "16x16 basesWorkers, every env vs device coacAI (k_bot), random masked agent actions",
+    "workerrush": "16x16 basesWorkers, every env vs device workerRushAI (k_bot), random masked agent actions",
+    "partial_obs": "16x16 basesWorkers selfplay, partial_obs=True (31 planes), random masked actions",
+    "8x8": "8x8 basesWorkers selfplay, random masked actions",
+    "24x24": "24x24 basesWorkers selfplay, random masked actions",
+}
+
+
+def shard(rank, n):
+    """rank r owns global envs [r*n, (r+1)*n); n even so selfplay pairs never straddle
+    ranks; the sampler seed is shard-specific."""
+    assert n % 2 == 0, "envs per GPU must be even (selfplay pairs)"
+    return rank * n, (rank + 1) * n
 
 
 def kernel_bytes(G, N, HW, P=29):
@@ -85,7 +116,14 @@ def run_gpu(args, rank, world, local_rank):
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     n = args.envs_per_gpu
-    env = MicroRTSGridModeVecEnv(num_selfplay_envs=n, num_bot_envs=0, max_steps=args.max_steps, map_paths=[MAP],
+    shard(rank, n)
+    from gym_microrts import microrts_ai
+
+    wmap, nsp, nbot, bot, po = WORKLOADS[args.workload]
+    nsp = n if nsp == "all" else nsp
+    nbot = n if nbot == "all" else nbot
+    env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
+                                 ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
                                  reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, return_tensors=True)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
@@ -122,8 +160,8 @@ def run_gpu(args, rank, world, local_rank):
     elapsed = t1 - t0
     flags = env.error_flags()
     kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
-    G = env.num_envs // 2
-    return elapsed, kern, flags, env.height * env.width, G, env.num_envs
+    G = nsp // 2 + nbot
+    return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes)
 
 
 def barrier(world, dev):
@@ -133,7 +171,8 @@ def barrier(world, dev):
 
         t = torch.ones(1, device=dev)
         dist.all_reduce(t)
-        torch.cuda.synchronize(dev)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
 
 def max_over_ranks(x, world, dev):
@@ -187,14 +226,14 @@ def main():
 
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    elapsed, kern, flags, hw, G, N = run_gpu(args, rank, world, local_rank)
+    elapsed, kern, flags, hw, G, N, P = run_gpu(args, rank, world, local_rank)
     dev = torch.device("cuda", local_rank)
     elapsed_max = max_over_ranks(elapsed, world, dev)
     total_env_steps = world * N * args.steps
     value = total_env_steps / elapsed_max
     out = None
     if rank == 0:
-        kb = kernel_bytes(G, N, hw)
+        kb = kernel_bytes(G, N, hw, P)
         roof = None
         kernels = {}
         for k, ms in kern.items():
@@ -212,7 +251,7 @@ def main():
                     "traffic": None if traffic is None else round(traffic / (kern[dom] * 1e-3) / 1e9, 1),
                     "traffic_bytes_per_launch": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": kb[dom], "kernel": dom, "avg_launch_ms": round(kern[dom], 4)}
-        env_step_bytes = hw * (4 * 29 + 312 + 56 + 32) + 64   # SURVEY.md §8d whole-step formula
+        env_step_bytes = hw * (4 * P + 312 + 56 + 32) + 64   # SURVEY.md §8d whole-step formula
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -226,17 +265,18 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
-            "config": {"workload": "16x16 basesWorkers selfplay, random masked actions (device Philox sampler), "
-                                   "get_action_mask+sample+step per env-step",
-                       "envs_per_gpu": N, "games_per_gpu": G, "map": MAP, "max_steps": args.max_steps,
-                       "obs": "float32 device tensor", "parallelism": f"env-shard x{world}"},
+            "config": {"workload": WORKLOAD_DESC[args.workload],
+                       "envs_per_gpu": N, "games_per_gpu": G, "map": WORKLOADS[args.workload][0], "max_steps": args.max_steps,
+                       "obs": f"float32 device tensor, {P} planes", "parallelism": f"env-shard x{world}"},
             "roofline": roof,
             "kernels": kernels,
             "env_step_bytes": env_step_bytes,
             "env_step_roofline_frac": round(value / world * env_step_bytes / (HBM_PEAK_GBS * 1e9), 4),
             "engine_error_flags": flags,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if args.workload != "selfplay":
+            out["metric"] = f"env-steps/sec, workload {args.workload} (secondary config, not the BASELINE metric)"
+        if world == 1 and not args.no_cpu_baseline and args.workload == "selfplay":
             out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
