@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "mrts_engine.h"
 #include "mrts_layout.h"
 
@@ -715,59 +717,76 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
     }
 }
 
-// One workgroup = SR consecutive (env, cell) rows.  The rows' 78-int32 masks
-// (SR*312 B, contiguous) are streamed with coalesced 16-byte loads and folded
-// into 78-bit words in LDS; each lane then samples its row and the 7 int64
-// components are staged in LDS and written back with coalesced 16-byte stores.
-constexpr int SR = 256;
+// Persistent, software-pipelined: every WAVE owns groups of SW = 32 consecutive
+// (env, cell) rows (32 x 312 B of int32 mask, contiguous).  While a group is
+// folded into 78-bit words in the wave's LDS slice and sampled (one lane per
+// row), the NEXT group's 10 dwordx4 loads per lane are already in flight in a
+// second register buffer, so the HBM stream never idles behind the Philox /
+// selection arithmetic.  The 7 int64 components per row are staged in LDS and
+// written back with coalesced 16-byte stores.  No block barriers: a wave's own
+// LDS operations complete in order.
+constexpr int SW = 32;                                   // rows per group (one wave)
+constexpr int SWAVES = 4;                                // waves per workgroup
+constexpr int SNV = (SW * MRTS_MASK_CH / 4 + 63) / 64;   // dwordx4 loads per lane per group (10)
 
-__global__ __launch_bounds__(SR) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed, uint32_t step,
-                                               int64_t* __restrict__ act) {
-    __shared__ uint32_t s_bits[SR * 3];
-    __shared__ __attribute__((aligned(16))) int64_t s_out[SR * 7];
-    const long long rows = (long long)n * hw;
-    const long long row0 = (long long)blockIdx.x * SR;
-    const int rb = (int)min((long long)SR, rows - row0);
-    for (int i = threadIdx.x; i < SR * 3; i += SR) s_bits[i] = 0;
-    __syncthreads();
-    const int32_t* mb = mask + row0 * MRTS_MASK_CH;   // 16-B aligned: SR*312 B per block
-    const int nel = rb * MRTS_MASK_CH, nv = nel >> 2;
-    const int4* m4 = reinterpret_cast<const int4*>(mb);
-    // issue every load of the block's mask rows before consuming any (the LDS
-    // atomics below would otherwise serialise one HBM round trip per load)
-    constexpr int NV = (SR * MRTS_MASK_CH / 4 + SR - 1) / SR;
-    int4 vbuf[NV];
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+struct SampleBuf {
+    int4 v[SNV];
+};
+
+__device__ __forceinline__ void sample_load(SampleBuf& B, const int32_t* __restrict__ mask, long long grp, long long rows) {
+    const long long row0 = grp * SW;
+    const int rb = (int)min((long long)SW, rows - row0);
+    const int nv = rb * MRTS_MASK_CH / 4;
+    const int4* m4 = reinterpret_cast<const int4*>(mask + row0 * MRTS_MASK_CH);
 #pragma unroll
-    for (int j = 0; j < NV; j++) {
-        const int k = j * SR + threadIdx.x;
-        vbuf[j] = k < nv ? m4[k] : make_int4(0, 0, 0, 0);
+    for (int j = 0; j < SNV; j++) {
+        const int k = j * 64 + (threadIdx.x & 63);
+        if (k < nv) {   // streamed once: non-temporal (no L2 allocation)
+            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(m4 + k));
+            B.v[j] = make_int4(t.x, t.y, t.z, t.w);
+        } else {
+            B.v[j] = make_int4(0, 0, 0, 0);
+        }
     }
+}
+
+__device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* __restrict__ mask, long long grp, long long rows,
+                                             int hw, uint64_t seed, uint32_t step, int64_t* __restrict__ act,
+                                             uint32_t* s_bits, int64_t* s_out) {
+    const int lane = threadIdx.x & 63;
+    const long long row0 = grp * SW;
+    const int rb = (int)min((long long)SW, rows - row0);
+    const int nel = rb * MRTS_MASK_CH, nv = nel >> 2;
+    for (int i = lane; i < SW * 3; i += 64) s_bits[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-    for (int j = 0; j < NV; j++) {
-        const int k = j * SR + threadIdx.x;
-        const int4 v = vbuf[j];
+    for (int j = 0; j < SNV; j++) {
+        const int k = j * 64 + lane;
+        const int4 v = B.v[j];
         if (k >= nv || (v.x | v.y | v.z | v.w) == 0) continue;   // most cells hold no idle unit
         int e = 4 * k;
         int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
-        int vv[4] = {v.x, v.y, v.z, v.w};
+        const int vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (vv[j]) atomicOr(&s_bits[3 * r + (ch >> 5)], 1u << (ch & 31));
+        for (int q = 0; q < 4; q++) {
+            if (vv[q]) atomicOr(&s_bits[3 * r + (ch >> 5)], 1u << (ch & 31));
             if (++ch == MRTS_MASK_CH) { ch = 0; r++; }
         }
     }
-    for (int e = 4 * nv + threadIdx.x; e < nel; e += SR) {
-        if (mb[e]) {
+    for (int e = 4 * nv + lane; e < nel; e += 64) {   // odd row count: the last 2 int32
+        if (mask[row0 * MRTS_MASK_CH + e]) {
             int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
             atomicOr(&s_bits[3 * r + (ch >> 5)], 1u << (ch & 31));
         }
     }
-    __syncthreads();
-    if (threadIdx.x < rb) {
-        const long long idx = row0 + threadIdx.x;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane < rb) {
+        const long long idx = row0 + lane;
         const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
-        const uint64_t lo = (uint64_t)s_bits[3 * threadIdx.x] | ((uint64_t)s_bits[3 * threadIdx.x + 1] << 32);
-        const uint64_t hi = s_bits[3 * threadIdx.x + 2];
+        const uint64_t lo = (uint64_t)s_bits[3 * lane] | ((uint64_t)s_bits[3 * lane + 1] << 32);
+        const uint64_t hi = s_bits[3 * lane + 2];
         uint32_t r[8];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -779,8 +798,7 @@ __global__ __launch_bounds__(SR) void k_sample(const int32_t* __restrict__ mask,
         const int len[7] = {6, 4, 4, 4, 4, 7, 49};
 #pragma unroll
         for (int k = 0; k < 7; k++) {
-            // segment bits [off, off+len) of the 78-bit word
-            uint64_t seg = (lo >> off[k]) | (off[k] ? (hi << (64 - off[k])) : 0);
+            uint64_t seg = (lo >> off[k]) | (off[k] ? (hi << (64 - off[k])) : 0);   // bits [off, off+len)
             seg &= (1ull << len[k]) - 1ull;
             const int nvalid = __popcll(seg);
             int pick;
@@ -791,16 +809,42 @@ __global__ __launch_bounds__(SR) void k_sample(const int32_t* __restrict__ mask,
                 for (; t > 0; t--) seg &= seg - 1ull;   // drop the t lowest set bits
                 pick = __builtin_ctzll(seg);
             }
-            s_out[threadIdx.x * 7 + k] = pick;
+            s_out[lane * 7 + k] = pick;
         }
     }
-    __syncthreads();
-    int64_t* ob = act + row0 * 7;   // 16-B aligned: SR*56 B per block
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    int64_t* ob = act + row0 * 7;   // 16-B aligned: SW * 56 B per group
     const int onel = rb * 7, onv = onel >> 1;
     int4* o4 = reinterpret_cast<int4*>(ob);
     const int4* s4 = reinterpret_cast<const int4*>(s_out);
-    for (int k = threadIdx.x; k < onv; k += SR) o4[k] = s4[k];
-    if ((onel & 1) && threadIdx.x == 0) ob[onel - 1] = s_out[onel - 1];
+    for (int k = lane; k < onv; k += 64) o4[k] = s4[k];
+    if ((onel & 1) && lane == 0) ob[onel - 1] = s_out[onel - 1];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+__global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
+                                                        uint32_t step, int64_t* __restrict__ act) {
+    __shared__ uint32_t s_bits[SWAVES][SW * 3];
+    __shared__ __attribute__((aligned(16))) int64_t s_out[SWAVES][SW * 7];
+    const int w = threadIdx.x >> 6;
+    const long long rows = (long long)n * hw;
+    const long long ngrp = (rows + SW - 1) / SW;
+    const long long stride = (long long)gridDim.x * SWAVES;
+    long long grp = (long long)blockIdx.x * SWAVES + w;
+    if (grp >= ngrp) return;
+    SampleBuf A, B;
+    sample_load(A, mask, grp, rows);
+    while (true) {   // two groups per trip: A is consumed while B loads, then the reverse
+        const long long g1 = grp + stride;
+        if (g1 < ngrp) sample_load(B, mask, g1, rows);
+        sample_group(A, mask, grp, rows, hw, seed, step, act, s_bits[w], s_out[w]);
+        if (g1 >= ngrp) break;
+        const long long g2 = g1 + stride;
+        if (g2 < ngrp) sample_load(A, mask, g2, rows);
+        sample_group(B, mask, g1, rows, hw, seed, step, act, s_bits[w], s_out[w]);
+        if (g2 >= ngrp) break;
+        grp = g2;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -850,7 +894,10 @@ hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts:
 hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
     int total = n * hw;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(mrts::k_sample, dim3((total + mrts::SR - 1) / mrts::SR), dim3(mrts::SR), 0, s, mask, n, hw, seed, step, act);
+    // persistent grid: enough waves to keep every CU streaming, each looping over row groups
+    const long long groups = ((long long)total + mrts::SW - 1) / mrts::SW;
+    const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * 2);   // 2 blocks per CU resident
+    hipLaunchKernelGGL(mrts::k_sample, dim3((unsigned)blocks), dim3(64 * mrts::SWAVES), 0, s, mask, n, hw, seed, step, act);
     return hipGetLastError();
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {
