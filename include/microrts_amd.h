@@ -101,6 +101,14 @@ int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source);
 int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source,
               void *obs, double *raw_reward, uint8_t *done);
 
+/* Response.observation of the JNI client (vec_env.py:279-280, 1002-1003, 1035):
+ * GameState.getVectorObservation per env, int32 [N][P_raw][H][W], P_raw = 6
+ * (hp, resources, owner 1 = self / 2 = opponent, type id + 1, action type,
+ * terrain) + 1 visibility plane with partial obs.  The unencoded form of the
+ * obs mrts_reset / mrts_step write; for callers that keep the reference's own
+ * python _encode_obs. */
+int mrts_get_raw_obs(mrts_vec *h, void *stream, int32_t *raw);
+
 /* reward_weight and reward_shaping of MicroRTSGridModeVecEnv (vec_env.py:102-103,
  * 1003-1004, 1057), used by mrts_step_weighted.  Host array of 6 doubles. */
 int mrts_set_reward_weight(mrts_vec *h, const double *weight6, int32_t reward_shaping);

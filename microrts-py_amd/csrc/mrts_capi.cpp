@@ -343,6 +343,12 @@ int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
 }
 
+int mrts_get_raw_obs(mrts_vec *h, void *stream, int32_t *raw) {
+    if (!bound(h) || !raw) return fail(h, MRTS_ESTATE, "get_raw_obs: workspace not bound or raw null");
+    hipError_t e = mrts_engine_raw_obs(&h->base, (hipStream_t)stream, raw);
+    return e ? hip_fail(h, e, "raw obs launch") : MRTS_OK;
+}
+
 int mrts_set_reward_weight(mrts_vec *h, const double *w, int32_t shaping) {
     if (!h || !w) return fail(h, MRTS_EINVAL, "set_reward_weight: null argument");
     for (int k = 0; k < 6; k++) h->rw[k] = w[k];

@@ -38,6 +38,7 @@ hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t
 hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_bots(const EngineParams *p, hipStream_t s);
+hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *raw);
 hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);

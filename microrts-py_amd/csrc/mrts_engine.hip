@@ -271,6 +271,37 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
 }
 
 // ---------------------------------------------------------------------------
+// Raw observation kernel: Response.observation = GameState.getVectorObservation
+// (player) as the JNI client returns it, int32 [N][P_raw][H][W] (P_raw = 6, or 7
+// with partial obs) -- the input of the reference's python _encode_obs
+// (vec_env.py:280, 1035).  Same per-cell rules as cell_onehot, unencoded.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_raw(EngineParams p, int32_t* raw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Lds L = carve(smem, p.HW, p.W, NT);
+    const int g = blockIdx.x, HW = p.HW;
+    load_game<NT>(p, L, g);
+    const Game G = game_of(p, g);
+    const int PR = p.partial_obs ? 7 : 6, nw = HW / 32 + 1;
+    if (p.partial_obs) compute_vis<NT>(p, L);
+    for (int v = 0; v < G.nviews; v++) {
+        int32_t* out = raw + (size_t)(G.env0 + v) * PR * HW;
+        for (int c = threadIdx.x; c < HW; c += NT) {
+            uint32_t u = L.unit[c], a = L.act[c];
+            if (p.partial_obs && u != 0 && u_owner(u) != v && !((L.vis[v * nw + (c >> 5)] >> (c & 31)) & 1u)) u = 0;
+            const int ow = u_owner(u);
+            out[0 * HW + c] = u ? u_hp(u) : 0;
+            out[1 * HW + c] = u ? u_res(u) : 0;
+            out[2 * HW + c] = (u && ow >= 0) ? (ow == v ? 1 : 2) : 0;
+            out[3 * HW + c] = u ? u_type(u) + 1 : 0;
+            out[4 * HW + c] = (u && a) ? code_type(act_code(a)) : 0;
+            out[5 * HW + c] = L.wall[c];
+            if (p.partial_obs) out[6 * HW + c] = (u && ((L.vis[(1 - v) * nw + (c >> 5)] >> (c & 31)) & 1u)) ? 1 : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Mask kernel: JNIGridnetVecClient.getMasks(0) -> [N][HW][78] + source [N][HW]
 template <int NT>
 __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
@@ -890,6 +921,14 @@ hipError_t mrts_engine_reset(const EngineParams* p, hipStream_t s, const int32_t
     return mrts::dispatch(*p, 0, s, games, maps, count);
 }
 hipError_t mrts_engine_masks(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 1, s, nullptr, nullptr, 0); }
+hipError_t mrts_engine_raw_obs(const EngineParams* p, hipStream_t s, int32_t* raw) {
+    const int NT = p->HW <= 64 ? 64 : p->HW <= 128 ? 128 : 256;
+    const size_t sh = mrts_engine_lds_bytes(p->HW, p->W);
+    if (NT == 64) hipLaunchKernelGGL(mrts::k_raw<64>, dim3(p->G), dim3(64), sh, s, *p, raw);
+    else if (NT == 128) hipLaunchKernelGGL(mrts::k_raw<128>, dim3(p->G), dim3(128), sh, s, *p, raw);
+    else hipLaunchKernelGGL(mrts::k_raw<256>, dim3(p->G), dim3(256), sh, s, *p, raw);
+    return hipGetLastError();
+}
 hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 2, s, nullptr, nullptr, 0); }
 hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
     int total = n * hw;

@@ -69,6 +69,7 @@ SIGNATURES = {
     "mrts_reset": (ctypes.c_int, [P, P, P]),
     "mrts_get_masks": (ctypes.c_int, [P, P, P, P]),
     "mrts_step": (ctypes.c_int, [P, P, P, P, P, P, P]),
+    "mrts_get_raw_obs": (ctypes.c_int, [P, P, P]),
     "mrts_set_reward_weight": (ctypes.c_int, [P, P, ctypes.c_int32]),
     "mrts_step_weighted": (ctypes.c_int, [P, P, P, P, P, P, P, P, P]),
     "mrts_reset_games": (ctypes.c_int, [P, P, P, P, ctypes.c_int32, P]),
