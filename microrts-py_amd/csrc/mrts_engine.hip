@@ -46,6 +46,7 @@ struct Lds {
     uint8_t* wall;
     unsigned long long* ballot;
     uint32_t* posbits;
+    uint32_t* claim;   // [2][posw] target positions claimed by >= 1 / >= 2 rows this tick
     uint32_t* vis;   // [2][HW/32+1] cells observable by player 0 / 1 (partial obs)
     int* sc;         // scalars
 };
@@ -67,6 +68,7 @@ __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     b += a16(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     b += a16(4 * SC_WORDS);
     b += a16(8 * (size_t)(HW / 32 + 1));
+    b += a16(8 * (size_t)((HW + 2 * W) / 32 + 1));
     return b;
 }
 
@@ -90,6 +92,7 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     L.posbits = (uint32_t*)take(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     L.sc = (int*)take(4 * SC_WORDS);
     L.vis = (uint32_t*)take(8 * (size_t)(HW / 32 + 1));
+    L.claim = (uint32_t*)take(8 * (size_t)((HW + 2 * W) / 32 + 1));
     return L;
 }
 
@@ -352,6 +355,10 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
 // ---------------------------------------------------------------------------
 // Step kernel: JNIGridnetVecClient.gameStep for one game per workgroup.
 enum : uint32_t { CAND = 1u << 31, LEGAL = 1u << 30 };
+__device__ __forceinline__ int unchecked_pos(const Grid& gd, int c, int dir) {   // UnitAction.resourceUsage position
+    const int off[4] = {-gd.W, 1, gd.W, -1};
+    return c + off[dir];
+}
 
 __device__ __forceinline__ int res_of(const Lds& L, int player) { return L.sc[SC_RES0 + player]; }
 
@@ -475,8 +482,11 @@ __device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd
     }
 }
 
-// UnitAction.execute for one ready assignment (lane 0), from its snapshot
-__device__ void execute_one(const Lds& L, const Grid& gd, int4 s) {
+// UnitAction.execute for one ready assignment, from its snapshot.  Serial
+// (lane 0, issue order) or, for an independent ready set, one lane per action
+// (PAR: resource / error updates are atomic, the produced unit's id is given).
+template <bool PAR = false>
+__device__ void execute_one(const Lds& L, const Grid& gd, int4 s, int produced_uid = -1) {
     const int c = s.x;
     const uint32_t u = (uint32_t)s.y;
     const int code = (int)(s.z);
@@ -488,7 +498,11 @@ __device__ void execute_one(const Lds& L, const Grid& gd, int4 s) {
     case A_MOVE: {
         if (!here) break;
         int n = nb_cell(gd, c, param);
-        if (n < 0 || L.unit[n] != 0) { L.sc[SC_ERR] |= MRTS_ERR_MOVE_OCCUPIED; break; }
+        if (n < 0 || L.unit[n] != 0) {
+            if (PAR) atomicOr(&L.sc[SC_ERR], MRTS_ERR_MOVE_OCCUPIED);
+            else L.sc[SC_ERR] |= MRTS_ERR_MOVE_OCCUPIED;
+            break;
+        }
         L.unit[n] = L.unit[c];
         L.uid[n] = uid;
         L.act[n] = 0;
@@ -539,19 +553,25 @@ __device__ void execute_one(const Lds& L, const Grid& gd, int4 s) {
         if (n < 0) break;
         uint32_t o = L.unit[n];
         if (o == 0 || !ut_is_stockpile(u_type(o)) || u_res(u) <= 0) break;
-        L.sc[SC_RES0 + owner] += u_res(u);
+        if (PAR) atomicAdd(&L.sc[SC_RES0 + owner], u_res(u));
+        else L.sc[SC_RES0 + owner] += u_res(u);
         if (here) L.unit[c] = u_with_res(L.unit[c], 0);
         break;
     }
     case A_PRODUCE: {
         int n = nb_cell(gd, c, param);
         int put = code_utype(code);
-        if (n < 0 || L.unit[n] != 0) { L.sc[SC_ERR] |= MRTS_ERR_PRODUCE_OCCUPIED; break; }
+        if (n < 0 || L.unit[n] != 0) {
+            if (PAR) atomicOr(&L.sc[SC_ERR], MRTS_ERR_PRODUCE_OCCUPIED);
+            else L.sc[SC_ERR] |= MRTS_ERR_PRODUCE_OCCUPIED;
+            break;
+        }
         L.unit[n] = u_make(put, owner, ut_hp(put), 0);
-        L.uid[n] = L.sc[SC_UID]++;
+        L.uid[n] = PAR ? produced_uid : L.sc[SC_UID]++;
         L.act[n] = 0;
         L.seq[n] = 0;
-        L.sc[SC_RES0 + owner] -= ut_cost(put);
+        if (PAR) atomicSub(&L.sc[SC_RES0 + owner], ut_cost(put));
+        else L.sc[SC_RES0 + owner] -= ut_cost(put);
         break;
     }
     default: break;
@@ -567,10 +587,20 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const Grid gd{p.W, p.H, HW};
     const Game G = game_of(p, g);
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
+    // the source-unit rows of this lane's first cell, fetched in the same round
+    // trip as the game state (the decode below needs both)
+    int src_pre[2] = {0, 0};
+    if ((int)threadIdx.x < HW)
+        for (int v = 0; v < G.nviews; v++) src_pre[v] = p.src[(size_t)(G.env0 + v) * HW + threadIdx.x];
     __syncthreads();
     load_game<NT>(p, L, g);
     const int time = L.sc[SC_TIME];
 
+#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 1   // phase-cost experiments (scripts/build_variants.sh)
+    __syncthreads();
+    store_game<NT>(p, L, g);
+    return;
+#endif
     // (1) decode the rows of every idle unit whose cell is in source_unit_mask
     //     (vec_env.py:972-974) + Unit.canExecuteAction, lane-parallel.
     for (int c = threadIdx.x; c < HW; c += NT) {
@@ -581,8 +611,11 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             int view = G.selfplay ? ow : (ow == 0 ? 0 : -1);
             if (view >= 0) {
                 const size_t row = (size_t)(G.env0 + view) * HW + c;
-                if (p.src[row]) {
-                    const int64_t* r = p.actions + row * 7;
+                if (c == (int)threadIdx.x ? src_pre[view] : p.src[row]) {
+                    const int64_t* ra = p.actions + row * 7;
+                    int64_t r[7];   // all 7 components in one round trip
+#pragma unroll
+                    for (int k = 0; k < 7; k++) r[k] = ra[k];
                     int64_t ty = r[0];
                     int code = -1;
                     if (ty == A_NONE) code = code_make(A_NONE, 1, 0);   // NONE(1): param = duration
@@ -631,6 +664,69 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         uint32_t a = L.act[c];
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
     }, L.prod, L.ballot);
+#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 2   // phase-cost experiments (scripts/build_variants.sh)
+    __syncthreads();
+    store_game<NT>(p, L, g);
+    return;
+#endif
+    // (2a) rows that interact with nothing else this tick issue lane-parallel: an
+    //      agent row that is not a produce and, if a move, whose target position
+    //      no other row (either player, bot rows included) and no pending
+    //      assignment claims, while no pending produce is over its owner's budget
+    //      (which would make every new action inconsistent).  Such a row meets no
+    //      candidate in issue() and no other row in fromVectorAction's filter, so
+    //      issuing it out of order is exact: its LinkedHashMap rank is still its
+    //      cell.  Everything else takes the ordered path (2b).
+    {
+        const int posw = (HW + 2 * p.W) / 32 + 1;
+        for (int i = threadIdx.x; i < 2 * posw; i += NT) L.claim[i] = 0;
+        int over = 0;
+        for (int k = threadIdx.x; k < nprod; k += NT) {
+            const int pc = L.prod[k];
+            over |= ut_cost(code_utype(act_code(L.act[pc]))) > res_of(L, u_owner(L.unit[pc]));
+        }
+        over = __syncthreads_or(over);
+        for (int c = threadIdx.x; c < HW; c += NT) {
+            const uint32_t nw = L.aux[c];
+            if (!(nw & CAND)) continue;
+            const int code = (int)(nw & 0xFFFu), ty = code_type(code);
+            if (ty != A_MOVE && ty != A_PRODUCE) continue;
+            const int b = unchecked_pos(gd, c, code_param(code)) + p.W;
+            const uint32_t bit = 1u << (b & 31);
+            if (atomicOr(&L.claim[b >> 5], bit) & bit) atomicOr(&L.claim[posw + (b >> 5)], bit);
+        }
+        __syncthreads();
+        if (!over) {
+            for (int c = threadIdx.x; c < HW; c += NT) {
+                const uint32_t nw = L.aux[c];
+                if (!(nw & CAND)) continue;
+                const uint32_t u = L.unit[c];
+                const int q = u_owner(u);
+                if (!G.selfplay && q != 0) continue;   // bot rows: ordered path
+                const int code = (int)(nw & 0xFFFu), ty = code_type(code);
+                if (ty == A_PRODUCE) continue;
+                int n = -1;
+                if (ty == A_MOVE) {
+                    const int b = unchecked_pos(gd, c, code_param(code)) + p.W;
+                    if ((L.claim[posw + (b >> 5)] >> (b & 31)) & 1u) continue;
+                    n = nb_cell(gd, c, code_param(code));
+                    if (n >= 0 && L.resv[n] >= 0) continue;
+                }
+                int cur = code, dur = 0;
+                if (ty == A_NONE) dur = code_param(code);
+                else if (!(nw & LEGAL)) { dur = eta_code(code, u_type(u)); cur = code_make(A_NONE, 0, 0); }
+                const int ct = code_type(cur);
+                L.act[c] = act_make(cur, ct == A_NONE ? time + dur : time + eta_code(cur, u_type(u)));
+                L.seq[c] = seq_make(time, q, c);
+                if (ct == A_MOVE) L.resv[n] = c;
+                if (ct == A_HARVEST || ct == A_RETURN) atomicAdd(&L.sc[SC_R0 + 6 * q + 1], 1);
+                if (ct == A_ATTACK) atomicAdd(&L.sc[SC_R0 + 6 * q + 4], 1);
+                L.aux[c] = nw & ~CAND;   // issued
+            }
+            __syncthreads();
+        }
+    }
+    // (2b) the ordered path for the rest
     int nrows = compact_cells<NT>(HW, [&](int c) { return (L.aux[c] & CAND) != 0; }, L.list, L.ballot);
     // (2) ordered part: p0 then p1 (bot envs: the passive bot issues only NONEs)
     if (threadIdx.x == 0) {
@@ -640,6 +736,11 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         else if (npa > 0) issue_player(p, L, gd, 1, L.blist, npa, false);
     }
     __syncthreads();
+#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 3   // phase-cost experiments (scripts/build_variants.sh)
+    __syncthreads();
+    store_game<NT>(p, L, g);
+    return;
+#endif
     // (3) fillWithNones(gs, player, 1) for every idle unit (both players)
     for (int c = threadIdx.x; c < HW; c += NT) {
         uint32_t u = L.unit[c];
@@ -659,33 +760,61 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         uint32_t a = L.act[c];
         return a != 0 && act_done(a) <= now;
     }, L.list, L.ballot);
+    // snapshots of the ready assignments in LinkedHashMap (issue-sequence)
+    // order: lane-parallel rank by sequence word (unique among non-NONE actions)
+    const int posw = (HW + 2 * p.W) / 32 + 1;
+    for (int i = threadIdx.x; i < posw; i += NT) L.claim[i] = 0;
+    for (int i = threadIdx.x; i < nready; i += NT) {
+        const int c = L.list[i];
+        const uint32_t sq = L.seq[c];
+        int rank = 0;
+        for (int j = 0; j < nready; j++) rank += L.seq[L.list[j]] < sq;
+        L.snap[rank] = make_int4(c, (int)L.unit[c], act_code(L.act[c]), L.uid[c]);
+    }
+    __syncthreads();
+    // Independent ready sets (no attack, no two harvests of one pile) commute:
+    // every target cell is distinct (moves / produces hold reservations),
+    // resources only add up, and produced units take ids in issue order.
+    int serial = 0;
+    for (int i = threadIdx.x; i < nready; i += NT) {
+        L.act[L.list[i]] = 0;   // unitActions.remove
+        const int4 sn = L.snap[i];
+        const int ty = code_type(sn.z);
+        if (ty == A_ATTACK) serial = 1;
+        if (ty == A_HARVEST) {
+            const int n = nb_cell(gd, sn.x, code_param(sn.z));
+            if (n >= 0 && (atomicOr(&L.claim[n >> 5], 1u << (n & 31)) >> (n & 31)) & 1u) serial = 1;
+        }
+    }
+    serial = __syncthreads_or(serial);
+    if (serial) {
+        if (threadIdx.x == 0)
+            for (int i = 0; i < nready; i++) execute_one(L, gd, L.snap[i]);
+    } else {
+        for (int i = threadIdx.x; i < nready; i += NT) {
+            const int4 sn = L.snap[i];
+            int puid = -1;
+            if (code_type(sn.z) == A_PRODUCE) {
+                puid = L.sc[SC_UID];
+                for (int j = 0; j < i; j++) puid += code_type(L.snap[j].z) == A_PRODUCE;
+            }
+            execute_one<true>(L, gd, sn, puid);
+        }
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         L.sc[SC_TIME] = now;
         L.sc[SC_TICKS]++;
         if (now >= MRTS_MAX_TIME) L.sc[SC_ERR] |= MRTS_ERR_TIME_OVERFLOW;
-        if (nready > 0) {
-            for (int i = 0; i < nready; i++) {
-                int c = L.list[i];
-                L.snap[i] = make_int4(c, (int)L.unit[c], act_code(L.act[c]), L.uid[c]);
-                L.resv[i] = (int)L.seq[c];
-            }
-            for (int i = 0; i < nready; i++) L.act[L.list[i]] = 0;   // unitActions.remove
-            for (int a = 1; a < nready; a++) {                      // LinkedHashMap order
-                int4 x = L.snap[a];
-                int xs = L.resv[a];
-                int b = a - 1;
-                while (b >= 0 && (uint32_t)L.resv[b] > (uint32_t)xs) {
-                    L.snap[b + 1] = L.snap[b];
-                    L.resv[b + 1] = L.resv[b];
-                    b--;
-                }
-                L.snap[b + 1] = x;
-                L.resv[b + 1] = xs;
-            }
-            for (int i = 0; i < nready; i++) execute_one(L, gd, L.snap[i]);
-        }
+        if (!serial)
+            for (int i = 0; i < nready; i++) L.sc[SC_UID] += code_type(L.snap[i].z) == A_PRODUCE;
     }
     __syncthreads();
+#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 4   // phase-cost experiments (scripts/build_variants.sh)
+    __syncthreads();
+    store_game<NT>(p, L, g);
+    return;
+#endif
     // (5) PhysicalGameState.gameover / winner
     int has0 = 0, has1 = 0;
     for (int c = threadIdx.x; c < HW; c += NT) {
@@ -728,8 +857,10 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     __syncthreads();
     // (7) write back + one-hot observation of every view
     store_game<NT>(p, L, g);
+#ifndef MRTS_EXP_NOOBS   // kernel-variant experiments only (scripts/kernel_variants.py)
     if (P == 31) compute_vis<NT>(p, L);
     for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -853,7 +984,13 @@ __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* 
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
-__global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
+#ifndef MRTS_SAMPLE_MIN_WAVES
+#define MRTS_SAMPLE_MIN_WAVES 1
+#endif
+#ifndef MRTS_SAMPLE_BLOCKS_PER_CU
+#define MRTS_SAMPLE_BLOCKS_PER_CU 2
+#endif
+__global__ __launch_bounds__(64 * SWAVES, MRTS_SAMPLE_MIN_WAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
                                                         uint32_t step, int64_t* __restrict__ act) {
     __shared__ uint32_t s_bits[SWAVES][SW * 3];
     __shared__ __attribute__((aligned(16))) int64_t s_out[SWAVES][SW * 7];
@@ -935,7 +1072,7 @@ hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed,
     if (total == 0) return hipSuccess;
     // persistent grid: enough waves to keep every CU streaming, each looping over row groups
     const long long groups = ((long long)total + mrts::SW - 1) / mrts::SW;
-    const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * 2);   // 2 blocks per CU resident
+    const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * MRTS_SAMPLE_BLOCKS_PER_CU);   // resident blocks
     hipLaunchKernelGGL(mrts::k_sample, dim3((unsigned)blocks), dim3(64 * mrts::SWAVES), 0, s, mask, n, hw, seed, step, act);
     return hipGetLastError();
 }
