@@ -67,6 +67,9 @@ typedef struct {
     const int32_t *game_map;     /* [num_games] index into map_paths, NULL -> 0      */
     const int32_t *bot_ai;       /* [num_bot_envs] MRTS_AI_*, NULL -> passive        */
     int32_t obs_dtype;           /* MRTS_OBS_INT32 (reference dtype) or FLOAT32      */
+    const int32_t *bot_ai0;      /* [num_bot_envs] MRTS_AI_* of player 0 (bot vs bot,
+                                    MicroRTSBotVecEnv / JNIBotClient, vec_env.py:1104-1236),
+                                    -1 = the agent plays player 0; NULL = all agent */
 } mrts_config;
 
 typedef struct {

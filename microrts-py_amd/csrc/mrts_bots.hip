@@ -650,7 +650,7 @@ __device__ void random_biased_get_action(BS& S, const BL& L) {
         if (u_owner(u) != S.player || L.act[c] != 0) continue;
         int total = 0;
         unit_actions(S, L, c, [&](int, int w) { total += w; });
-        uint32_t ctr[4] = {(uint32_t)L.uid[c], S.tick, (uint32_t)S.game, 0x52414E44u};
+        uint32_t ctr[4] = {(uint32_t)L.uid[c], S.tick, (uint32_t)S.game, 0x52414E44u + (uint32_t)(1 - S.player)};
         philox_b(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
         int t = (int)(((uint64_t)ctr[0] * (uint32_t)total) >> 32), pick = -1;
         unit_actions(S, L, c, [&](int code, int w) {
@@ -669,26 +669,32 @@ __device__ void random_biased_get_action(BS& S, const BL& L) {
 // ---- the kernel ------------------------------------------------------------------------
 __global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int b = blockIdx.x, g = p.nsp_games + b, lane = threadIdx.x;
+    // blockIdx.y = the bot's player: 1 = ai2 (every bot env), 0 = ai1 of a
+    // bot-vs-bot game (MicroRTSBotVecEnv); both see the same pre-issue state
+    const int b = blockIdx.x, g = p.nsp_games + b, lane = threadIdx.x, player = gridDim.y == 2 ? (int)blockIdx.y : 1;
     const int HW = p.HW, W = p.W;
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
+    const int w_aa = player ? MRTS_G_AA_N : MRTS_G_AA_N0, w_npa = player ? MRTS_G_NPA : MRTS_G_NPA0;
     BS S;
-    S.ai = p.bot_ai[b];
+    S.ai = player ? p.bot_ai[b] : (p.bot_ai0 ? p.bot_ai0[b] : -1);
+    if (S.ai < 0) return;            // the agent plays this side
     if (S.ai == MRTS_AI_PASSIVE) {   // PassiveAI: all NONE (k_step's fill)
-        if (lane0()) genv[MRTS_G_NPA] = 0;
+        if (lane0()) genv[w_npa] = 0;
         return;
     }
     BL L = bot_carve(smem, HW, W);
+    int4* const aa_g = p.aa + ((size_t)b * 2 + player) * HW * 2;
+    int32_t* const pa_g = p.botpa + ((size_t)b * 2 + player) * HW;
     S.W = W;
     S.H = p.H;
     S.HW = HW;
-    S.player = 1;
+    S.player = player;
     S.partial = p.partial_obs;
     S.game = g;
     S.tick = (uint32_t)genv[MRTS_G_TICKS];
     S.res[0] = genv[MRTS_G_RES0];
     S.res[1] = genv[MRTS_G_RES1];
-    S.naa = genv[MRTS_G_AA_N];
+    S.naa = genv[w_aa];
     S.npa = 0;
     S.pa_res[0] = S.pa_res[1] = 0;
     const int map = genv[MRTS_G_MAP];
@@ -702,7 +708,7 @@ __global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
     }
     for (int i = lane; i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
     for (int i = lane; i < visw; i += BT) L.vis[i] = 0;
-    for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = p.aa[(size_t)b * HW * 2 + i];
+    for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
     if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     __syncthreads();
     // cells observable by the bot's player (PartiallyObservableGameState)
@@ -780,12 +786,12 @@ __global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
     default: break;
     }
     __syncthreads();
-    for (int i = lane; i < S.npa; i += BT) p.botpa[(size_t)b * HW + i] = L.pa[i];
-    for (int i = lane; i < 2 * S.naa; i += BT) p.aa[(size_t)b * HW * 2 + i] = L.aa[i];
+    for (int i = lane; i < S.npa; i += BT) pa_g[i] = L.pa[i];
+    for (int i = lane; i < 2 * S.naa; i += BT) aa_g[i] = L.aa[i];
     if (lane0()) {
-        genv[MRTS_G_NPA] = S.npa;
-        genv[MRTS_G_AA_N] = S.naa;
-        genv[MRTS_G_ERR] |= L.sc[2];
+        genv[w_npa] = S.npa;
+        genv[w_aa] = S.naa;
+        if (L.sc[2]) atomicOr(&genv[MRTS_G_ERR], L.sc[2]);
     }
 }
 
@@ -795,7 +801,7 @@ extern "C" {
 hipError_t mrts_engine_bots(const EngineParams* p, hipStream_t s) {
     const int nb = p->G - p->nsp_games;
     if (nb <= 0 || p->nbot_active == 0) return hipSuccess;
-    hipLaunchKernelGGL(mrts::k_bot, dim3(nb), dim3(mrts::BT), mrts::bot_lds_bytes(p->HW, p->W), s, *p);
+    hipLaunchKernelGGL(mrts::k_bot, dim3(nb, p->bot_ai0 ? 2 : 1), dim3(mrts::BT), mrts::bot_lds_bytes(p->HW, p->W), s, *p);
     return hipGetLastError();
 }
 size_t mrts_engine_bot_lds_bytes(int HW, int W) { return mrts::bot_lds_bytes(HW, W); }

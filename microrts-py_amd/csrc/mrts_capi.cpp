@@ -156,9 +156,11 @@ struct mrts_vec {
     std::vector<MapData> maps;
     std::vector<int32_t> game_map;
     std::vector<int32_t> bot_ai;
+    std::vector<int32_t> bot_ai0;   // -1: the agent plays player 0
+    int nbot0 = 0;
     // workspace carving
     size_t off_cells = 0, off_genv = 0, off_mcells = 0, off_mwall = 0, off_mscal = 0, off_scratch = 0, total = 0;
-    size_t off_botai = 0, off_aa = 0, off_botpa = 0;
+    size_t off_botai = 0, off_botai0 = 0, off_aa = 0, off_botpa = 0;
     int nbot_active = 0;
     unsigned char *ws = nullptr;
     std::vector<int32_t> scratch_host;
@@ -225,6 +227,15 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
         h->bot_ai[j] = a;
         h->nbot_active += a != MRTS_AI_PASSIVE;
     }
+    h->bot_ai0.assign(h->nbot, -1);
+    h->nbot0 = 0;
+    for (int j = 0; cfg->bot_ai0 && j < h->nbot; j++) {
+        int a = cfg->bot_ai0[j];
+        if (a < -1 || a >= MRTS_AI_COUNT) return fail(h, MRTS_EINVAL, "bot_ai0: unknown MRTS_AI_* id");
+        h->bot_ai0[j] = a;
+        h->nbot0 += a >= 0;
+        h->nbot_active += a > MRTS_AI_PASSIVE;
+    }
     if (h->nbot_active) {
         if (h->W > 32 || h->H > 64)
             return fail(h, MRTS_ENOTIMPL, "device bots need maps at most 32 wide and 64 high (one bit word per row)");
@@ -239,8 +250,9 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     h->off_mscal = o; o = align256(o + (size_t)cfg->num_maps * MRTS_MAP_SCALARS * sizeof(int32_t));
     h->off_scratch = o; o = align256(o + (size_t)2 * h->ngames * sizeof(int32_t));
     h->off_botai = o; o = align256(o + (size_t)(h->nbot + 1) * sizeof(int32_t));
-    h->off_aa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * h->HW * 2 * sizeof(int4) : 0));
-    h->off_botpa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * h->HW * sizeof(int32_t) : 0));
+    h->off_botai0 = o; o = align256(o + (size_t)(h->nbot + 1) * sizeof(int32_t));
+    h->off_aa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * 2 * h->HW * 2 * sizeof(int4) : 0));
+    h->off_botpa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * 2 * h->HW * sizeof(int32_t) : 0));
     h->total = o;
     h->err.clear();
     return MRTS_OK;
@@ -283,6 +295,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
         (e = hipMemcpyAsync(h->ws + h->off_mscal, ms.data(), ms.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) ||
         (e = hipMemcpyAsync(h->ws + h->off_genv, genv.data(), genv.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) ||
         (h->nbot && (e = hipMemcpyAsync(h->ws + h->off_botai, h->bot_ai.data(), h->nbot * sizeof(int32_t), hipMemcpyHostToDevice, s))) ||
+        (h->nbot && (e = hipMemcpyAsync(h->ws + h->off_botai0, h->bot_ai0.data(), h->nbot * sizeof(int32_t), hipMemcpyHostToDevice, s))) ||
         (e = hipStreamSynchronize(s)))
         return hip_fail(h, e, "bind_workspace upload");
     EngineParams &p = h->base;
@@ -302,6 +315,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.obs_float = h->obs_float;
     p.partial_obs = h->partial_obs;
     p.bot_ai = (const int32_t *)(h->ws + h->off_botai);
+    p.bot_ai0 = h->nbot0 ? (const int32_t *)(h->ws + h->off_botai0) : nullptr;
     p.aa = h->nbot_active ? (int4 *)(h->ws + h->off_aa) : nullptr;
     p.botpa = h->nbot_active ? (int32_t *)(h->ws + h->off_botpa) : nullptr;
     p.nbot_active = h->nbot_active;

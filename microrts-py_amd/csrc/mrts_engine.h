@@ -27,10 +27,11 @@ struct EngineParams {
     double rw[6];
     int shaping;
     // device bots (mrts_bots.hip): bot game b = game nsp_games + b
-    const int32_t *bot_ai;  // [Gb] MRTS_AI_*
-    int4 *aa;               // [Gb][HW][2] AbstractionLayerAI.actions
-    int32_t *botpa;         // [Gb][HW] bot PlayerAction, cell | code << 16; null = none
-    int nbot_active;        // bot games whose AI is not passiveAI
+    const int32_t *bot_ai;  // [Gb] MRTS_AI_* of player 1
+    const int32_t *bot_ai0; // [Gb] MRTS_AI_* of player 0 in bot-vs-bot games, -1 = the agent
+    int4 *aa;               // [Gb][2][HW][2] AbstractionLayerAI.actions per bot player
+    int32_t *botpa;         // [Gb][2][HW] bot PlayerActions, cell | code << 16; null = none
+    int nbot_active;        // bot players (either side) whose AI is not passiveAI
 };
 
 extern "C" {

@@ -41,6 +41,7 @@ struct Lds {
     int32_t* list;   // compact cell lists
     int32_t* prod;   // pending produce cells
     int32_t* blist;  // the bot's PlayerAction order (bot games)
+    int32_t* blist0; // player 0's bot PlayerAction (bot-vs-bot games)
     int4* snap;      // ready-action snapshots
     uint32_t* mbits; // mask bits, 3 words per cell (mask kernel)
     uint8_t* wall;
@@ -60,7 +61,7 @@ __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15;
 
 __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     size_t b = 0;
-    b += a16(4 * (size_t)HW) * 9;  // unit uid act seq aux resv list prod + spare
+    b += a16(4 * (size_t)HW) * 10; // unit uid act seq aux resv list prod blist blist0
     b += a16(16 * (size_t)HW);     // snap
     b += a16(12 * (size_t)HW);     // mbits
     b += a16((size_t)HW);          // wall
@@ -85,6 +86,7 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     L.list = (int32_t*)take(4 * (size_t)HW);
     L.prod = (int32_t*)take(4 * (size_t)HW);
     L.blist = (int32_t*)take(4 * (size_t)HW);
+    L.blist0 = (int32_t*)take(4 * (size_t)HW);
     L.snap = (int4*)take(16 * (size_t)HW);
     L.mbits = (uint32_t*)take(12 * (size_t)HW);
     L.wall = (uint8_t*)take((size_t)HW);
@@ -595,12 +597,9 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     __syncthreads();
     load_game<NT>(p, L, g);
     const int time = L.sc[SC_TIME];
+    // bot-vs-bot game (MicroRTSBotVecEnv): player 0's PlayerAction comes from k_bot too
+    const bool bot0 = !G.selfplay && p.bot_ai0 && p.bot_ai0[g - p.nsp_games] >= 0;
 
-#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 1   // phase-cost experiments (scripts/build_variants.sh)
-    __syncthreads();
-    store_game<NT>(p, L, g);
-    return;
-#endif
     // (1) decode the rows of every idle unit whose cell is in source_unit_mask
     //     (vec_env.py:972-974) + Unit.canExecuteAction, lane-parallel.
     for (int c = threadIdx.x; c < HW; c += NT) {
@@ -608,7 +607,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         int ow = u_owner(u);
         L.resv[c] = -1;
         if (u != 0 && ow >= 0 && L.act[c] == 0) {
-            int view = G.selfplay ? ow : (ow == 0 ? 0 : -1);
+            int view = G.selfplay ? ow : (ow == 0 && !bot0 ? 0 : -1);
             if (view >= 0) {
                 const size_t row = (size_t)(G.env0 + view) * HW + c;
                 if (c == (int)threadIdx.x ? src_pre[view] : p.src[row]) {
@@ -642,11 +641,13 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // the device bot's PlayerAction for player 1 (k_bot, computed on the state
     // before this tick's issues: JNIGridnetClient.gameStep order)
     const int npa = (!G.selfplay && p.botpa) ? L.sc[SC_NPA] : 0;
-    for (int i = threadIdx.x; i < npa; i += NT) {
-        const int e = p.botpa[(size_t)(g - p.nsp_games) * HW + i];
+    const int npa0 = bot0 ? L.sc[MRTS_G_NPA0] : 0;
+    for (int i = threadIdx.x; i < npa + npa0; i += NT) {
+        const int q = i < npa ? 1 : 0, k = q ? i : i - npa;
+        const int e = p.botpa[((size_t)(g - p.nsp_games) * 2 + q) * HW + k];
         const int c = e & 0xFFFF, code = e >> 16;
-        L.blist[i] = c;
-        L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, 1)) ? LEGAL : 0u) | (uint32_t)code;
+        (q ? L.blist : L.blist0)[k] = c;
+        L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, q)) ? LEGAL : 0u) | (uint32_t)code;
     }
     __syncthreads();
     // pending move/produce reservations (ResourceUsage of unitActions)
@@ -664,11 +665,6 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         uint32_t a = L.act[c];
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
     }, L.prod, L.ballot);
-#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 2   // phase-cost experiments (scripts/build_variants.sh)
-    __syncthreads();
-    store_game<NT>(p, L, g);
-    return;
-#endif
     // (2a) rows that interact with nothing else this tick issue lane-parallel: an
     //      agent row that is not a produce and, if a move, whose target position
     //      no other row (either player, bot rows included) and no pending
@@ -702,7 +698,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
                 if (!(nw & CAND)) continue;
                 const uint32_t u = L.unit[c];
                 const int q = u_owner(u);
-                if (!G.selfplay && q != 0) continue;   // bot rows: ordered path
+                if (!G.selfplay && (q != 0 || bot0)) continue;   // bot rows: ordered path
                 const int code = (int)(nw & 0xFFFu), ty = code_type(code);
                 if (ty == A_PRODUCE) continue;
                 int n = -1;
@@ -731,16 +727,12 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // (2) ordered part: p0 then p1 (bot envs: the passive bot issues only NONEs)
     if (threadIdx.x == 0) {
         L.sc[SC_NPROD] = nprod;
-        issue_player(p, L, gd, 0, L.list, nrows, true);
+        if (bot0) issue_player(p, L, gd, 0, L.blist0, npa0, false);
+        else issue_player(p, L, gd, 0, L.list, nrows, true);
         if (G.selfplay) issue_player(p, L, gd, 1, L.list, nrows, true);
         else if (npa > 0) issue_player(p, L, gd, 1, L.blist, npa, false);
     }
     __syncthreads();
-#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 3   // phase-cost experiments (scripts/build_variants.sh)
-    __syncthreads();
-    store_game<NT>(p, L, g);
-    return;
-#endif
     // (3) fillWithNones(gs, player, 1) for every idle unit (both players)
     for (int c = threadIdx.x; c < HW; c += NT) {
         uint32_t u = L.unit[c];
@@ -810,11 +802,6 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             for (int i = 0; i < nready; i++) L.sc[SC_UID] += code_type(L.snap[i].z) == A_PRODUCE;
     }
     __syncthreads();
-#if defined(MRTS_EXP_STOP) && MRTS_EXP_STOP == 4   // phase-cost experiments (scripts/build_variants.sh)
-    __syncthreads();
-    store_game<NT>(p, L, g);
-    return;
-#endif
     // (5) PhysicalGameState.gameover / winner
     int has0 = 0, has1 = 0;
     for (int c = threadIdx.x; c < HW; c += NT) {
@@ -849,7 +836,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     __syncthreads();
     if (reset) {
         reset_into_lds<NT>(p, L, L.sc[SC_MAP]);
-        if (threadIdx.x == 0) L.sc[SC_AA_N] = 0;   // ai2.reset()
+        if (threadIdx.x == 0) L.sc[SC_AA_N] = L.sc[MRTS_G_AA_N0] = 0;   // ai1 / ai2.reset()
         __syncthreads();
     } else if (threadIdx.x == 0) {
         L.sc[SC_STEPS] = steps;

@@ -8,8 +8,8 @@
 //   cells  int4  [G][HW]  .x unit word  .y unit insertion index (pgs.units order)
 //                         .z action word .w issue sequence (LinkedHashMap order)
 //   genv   int32 [G][GENV_WORDS]
-//   bot games only (mrts_bots.hip): aa int4 [Gb][HW][2] (the bot's abstract
-//   actions, LinkedHashMap order), botpa int32 [Gb][HW] (cell | code << 16)
+//   bot games only (mrts_bots.hip): aa int4 [Gb][2][HW][2] (each bot player's
+//   abstract actions, LinkedHashMap order), botpa int32 [Gb][2][HW] (cell | code << 16)
 //   maps   per map: template cells int4 [HW], terrain u8 [HW], scalars int32 [4]
 //
 // Unit word   : bits 0-3 type+1 (0 = empty) | 4-5 owner+1 (0 = none/resource)
@@ -34,7 +34,7 @@
  *   TICKS steps since creation (never reset; bot RNG counter)
  *   NPA   entries of the bot PlayerAction handed from k_bot to k_step */
 enum { MRTS_G_TIME = 0, MRTS_G_RES0, MRTS_G_RES1, MRTS_G_NEXT_UID, MRTS_G_STEPS, MRTS_G_MAP, MRTS_G_ERR, MRTS_G_AA_N,
-       MRTS_G_TICKS, MRTS_G_NPA, MRTS_GENV_WORDS = 16 };
+       MRTS_G_TICKS, MRTS_G_NPA, MRTS_G_AA_N0, MRTS_G_NPA0, MRTS_GENV_WORDS = 16 };   /* *0: player-0 bot (bot vs bot) */
 enum { MRTS_M_RES0 = 0, MRTS_M_RES1, MRTS_M_NUNITS, MRTS_M_PAD, MRTS_MAP_SCALARS };
 
 /* error bits recorded in genv[MRTS_G_ERR] (invariant violations) */

@@ -44,6 +44,7 @@ class Config(ctypes.Structure):
         ("game_map", ctypes.POINTER(ctypes.c_int32)),
         ("bot_ai", ctypes.POINTER(ctypes.c_int32)),
         ("obs_dtype", ctypes.c_int32),
+        ("bot_ai0", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 
@@ -108,7 +109,7 @@ def check(rc, handle=None, what="call"):
         raise cls(f"libmicrorts_amd {what} failed ({ERROR_NAMES.get(rc, rc)}): {msg}")
 
 
-def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, game_map, bot_ai, obs_dtype):
+def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, game_map, bot_ai, obs_dtype, bot_ai0=None):
     cfg = Config()
     cfg.num_selfplay_envs = num_selfplay_envs
     cfg.num_bot_envs = num_bot_envs
@@ -122,6 +123,9 @@ def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, g
     cfg.game_map = ctypes.cast(gm, ctypes.POINTER(ctypes.c_int32))
     cfg.bot_ai = ctypes.cast(ai, ctypes.POINTER(ctypes.c_int32))
     cfg.obs_dtype = obs_dtype
+    if bot_ai0 is not None:
+        a0 = (ctypes.c_int32 * max(1, len(bot_ai0)))(*bot_ai0)
+        cfg.bot_ai0 = ctypes.cast(a0, ctypes.POINTER(ctypes.c_int32))
     h = P()
     rc = lib().mrts_create(ctypes.byref(cfg), ctypes.byref(h))
     if rc != MRTS_OK:

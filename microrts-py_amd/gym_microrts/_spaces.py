@@ -8,7 +8,7 @@ this image, so a minimal stand-in with the attributes the drivers read
 import numpy as np
 
 try:  # pragma: no cover - depends on the environment
-    from gym.spaces import Box, MultiDiscrete  # noqa: F401
+    from gym.spaces import Box, Discrete, MultiDiscrete  # noqa: F401
 except Exception:  # gym absent
 
     class _Space:
@@ -51,3 +51,19 @@ except Exception:  # gym absent
 
         def __repr__(self):
             return f"MultiDiscrete({self.nvec})"
+
+    class Discrete(_Space):
+        """gym.spaces.Discrete(n) (MicroRTSBotVecEnv's dummy spaces, vec_env.py:1180-1181)"""
+
+        def __init__(self, n):
+            self.n = int(n)
+            super().__init__((), np.int64)
+
+        def sample(self):
+            return int(self.np_random.integers(self.n))
+
+        def contains(self, x):
+            return 0 <= int(x) < self.n
+
+        def __repr__(self):
+            return f"Discrete({self.n})"

@@ -1,1 +1,2 @@
 from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv  # noqa: F401
+from gym_microrts.envs.vec_env import MicroRTSBotVecEnv  # noqa: F401

@@ -29,7 +29,7 @@ import torch
 import gym_microrts
 from gym_microrts import _native
 from gym_microrts._native import MicroRTSError, MicroRTSNotImplemented
-from gym_microrts._spaces import Box, MultiDiscrete
+from gym_microrts._spaces import Box, Discrete, MultiDiscrete
 
 RF_NAMES = [
     "WinLossRewardFunction",
@@ -123,6 +123,7 @@ class MicroRTSGridModeVecEnv:
         device=None,
         return_tensors=False,
         obs_dtype=None,
+        _ai1s=None,
     ):
         # vec_env.py:110-127
         self.num_selfplay_envs = num_selfplay_envs
@@ -165,13 +166,18 @@ class MicroRTSGridModeVecEnv:
         game_map = [self._map_index[full[e]] for e in game_env]
 
         # opponents (vec_env.py:268): factories -> device bot ids
-        bot_ai = []
-        for f in ai2s:
-            d = f(None)
-            ai_id = getattr(d, "ai_id", None)
-            if ai_id is None:
-                raise MicroRTSNotImplemented(f"bot {d} has no device implementation")
-            bot_ai.append(ai_id)
+        def device_ids(factories):
+            ids = []
+            for f in factories:
+                d = f(None) if callable(f) else f
+                ai_id = getattr(d, "ai_id", None)
+                if ai_id is None:
+                    raise MicroRTSNotImplemented(f"bot {d} has no device implementation")
+                ids.append(ai_id)
+            return ids
+
+        bot_ai = device_ids(ai2s)
+        bot_ai0 = device_ids(_ai1s) if _ai1s is not None else None   # MicroRTSBotVecEnv: player-0 bots
 
         # device + return contract
         if device is None:
@@ -190,7 +196,8 @@ class MicroRTSGridModeVecEnv:
 
         # new JNIGridnetVecClient(...) (vec_env.py:256-276)
         self._h = _native.create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, self._map_table, game_map,
-                                 bot_ai, _native.MRTS_OBS_FLOAT32 if obs_dtype == torch.float32 else _native.MRTS_OBS_INT32)
+                                 bot_ai, _native.MRTS_OBS_FLOAT32 if obs_dtype == torch.float32 else _native.MRTS_OBS_INT32,
+                                 bot_ai0=bot_ai0)
         self._game_map = list(game_map)
         info = _native.info(self._h)
         assert (info.height, info.width) == (self.height, self.width)
@@ -375,3 +382,55 @@ class MicroRTSGridModeVecEnv:
             self.close()
         except Exception:
             pass
+
+
+class MicroRTSBotVecEnv(MicroRTSGridModeVecEnv):
+    """Bot vs bot (vec_env.py:1104-1236; league.py:236-245 plays its matches with
+    it): env j is a game of ai1s[j] (player 0) against ai2s[j] (player 1), both
+    device bots computed by k_bot on the same pre-issue state each tick
+    (JNIBotClient.gameStep).  Observations are the reference's dummy
+    np.ones((N, 2)); rewards / dones are player 0's."""
+
+    metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 150}
+
+    def __init__(
+        self,
+        ai1s=[],
+        ai2s=[],
+        partial_obs=False,
+        max_steps=2000,
+        render_theme=2,
+        map_paths="maps/10x10/basesTwoWorkers10x10.xml",
+        reward_weight=np.array([0.0, 1.0, 0.0, 0.0, 0.0, 5.0]),
+        autobuild=True,
+        jvm_args=[],
+        *,
+        device=None,
+    ):
+        assert len(ai1s) == len(ai2s), "for each environment, a microrts ai should be provided"
+        if isinstance(map_paths, str):
+            map_paths = [map_paths]
+        super().__init__(num_selfplay_envs=0, num_bot_envs=len(ai1s), partial_obs=partial_obs, max_steps=max_steps,
+                         render_theme=render_theme, ai2s=ai2s, map_paths=map_paths, reward_weight=reward_weight,
+                         device=device, _ai1s=ai1s)
+        self.ai1s = ai1s
+        self.observation_space = Discrete(2)
+        self.action_space = Discrete(2)
+
+    def reset(self):
+        """vec_env.py:1223-1226"""
+        super().reset()
+        return np.ones((self.num_envs, 2))
+
+    def step_async(self, actions):
+        """vec_env.py:1228-1229: the actions are not used"""
+        self._actions_in = self._actions
+
+    def step_wait(self):
+        """vec_env.py:1231-1235"""
+        self._launch("step", _native.lib().mrts_step, self._h, self._stream(), self._actions.data_ptr(), self._src.data_ptr(),
+                     self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
+        reward = self._raw.cpu().numpy()
+        done = self._done.cpu().numpy().astype(bool)
+        infos = [{"raw_rewards": item} for item in reward]
+        return np.ones((self.num_envs, 2)), reward @ self.reward_weight, done[:, 0], infos

@@ -103,6 +103,7 @@ struct OVec {
     int nmaps;
     int *game_map;
     int *bot_ai;
+    int *bot_ai0;   /* per bot env: ai1 of a bot-vs-bot game, -1 = the agent plays p0 */
     OGS *gs;
     int *env_steps; /* per game (selfplay pairs step together)                */
     uint32_t *ticks;/* per game: steps since creation (bot RNG counter)        */
@@ -736,7 +737,7 @@ static void unit_masks(const OGS *g, int player, int32_t *m) {
 
 /* ------------------------------------------------------------------------- */
 OVec *ovec_create(int num_selfplay, int num_bot, int max_steps, int partial_obs, const OMap *maps,
-                  int num_maps, const int32_t *game_map, const int32_t *bot_ai) {
+                  int num_maps, const int32_t *game_map, const int32_t *bot_ai, const int32_t *bot_ai0) {
     OVec *v = (OVec *)calloc(1, sizeof(OVec));
     v->nsp = num_selfplay;
     v->nbot = num_bot;
@@ -762,10 +763,12 @@ OVec *ovec_create(int num_selfplay, int num_bot, int max_steps, int partial_obs,
     for (int i = 0; i < v->ngames; i++) v->game_map[i] = game_map ? game_map[i] : 0;
     v->bot_ai = (int *)calloc(num_bot + 1, sizeof(int));
     for (int i = 0; i < num_bot; i++) v->bot_ai[i] = bot_ai ? bot_ai[i] : OAI_PASSIVE;
+    v->bot_ai0 = (int *)calloc(num_bot + 1, sizeof(int));
+    for (int i = 0; i < num_bot; i++) v->bot_ai0[i] = bot_ai0 ? bot_ai0[i] : -1;
     v->gs = (OGS *)calloc(v->ngames, sizeof(OGS));
     v->env_steps = (int *)calloc(v->ngames, sizeof(int));
     v->ticks = (uint32_t *)calloc(v->ngames, sizeof(uint32_t));
-    v->aam = (OAAMap *)calloc(v->ngames, sizeof(OAAMap));
+    v->aam = (OAAMap *)calloc(2 * (size_t)v->ngames, sizeof(OAAMap)); /* [game][player] */
     v->raw = (int32_t *)calloc((size_t)v->nenvs * (partial_obs ? 7 : 6) * v->W * v->H, sizeof(int32_t));
     return v;
 }
@@ -784,10 +787,11 @@ void ovec_destroy(OVec *v) {
     free(v->maps);
     free(v->game_map);
     free(v->bot_ai);
+    free(v->bot_ai0);
     free(v->gs);
     free(v->env_steps);
     free(v->ticks);
-    for (int i = 0; i < v->ngames; i++) free(v->aam[i].e);
+    for (int i = 0; i < 2 * v->ngames; i++) free(v->aam[i].e);
     free(v->aam);
     free(v->raw);
     free(v);
@@ -819,7 +823,7 @@ void ovec_reset_game(OVec *v, int game, int map_id) {
     v->game_map[game] = map_id;
     gs_load(&v->gs[game], &v->maps[map_id]);
     v->env_steps[game] = 0;
-    v->aam[game].n = 0; /* ai2.reset() */
+    v->aam[2 * game].n = v->aam[2 * game + 1].n = 0; /* ai1/ai2.reset() */
     game_obs(v, game);
 }
 
@@ -852,8 +856,12 @@ void ovec_step(OVec *v, const int64_t *actions, const int32_t *src, double *rewa
             jni_get_action(g, 1, actions + (size_t)(e0 + 1) * HW * 7, src + (size_t)(e0 + 1) * HW, &pa1);
             issue_safe(g, &pa1);
         } else { /* JNIGridnetClient.gameStep: both actions, then issue */
-            jni_get_action(g, 0, actions + (size_t)e0 * HW * 7, src + (size_t)e0 * HW, &pa0);
-            bot_get_action(g, v->bot_ai[gi - v->nsp / 2], v->partial_obs, gi, v->ticks[gi], &v->aam[gi], &pa1);
+            const int b = gi - v->nsp / 2;
+            if (v->bot_ai0[b] >= 0) /* JNIBotClient.gameStep: ai1.getAction(0), ai2.getAction(1) */
+                bot_get_action(g, v->bot_ai0[b], 0, v->partial_obs, gi, v->ticks[gi], &v->aam[2 * gi], &pa0);
+            else
+                jni_get_action(g, 0, actions + (size_t)e0 * HW * 7, src + (size_t)e0 * HW, &pa0);
+            bot_get_action(g, v->bot_ai[b], 1, v->partial_obs, gi, v->ticks[gi], &v->aam[2 * gi + 1], &pa1);
             issue_safe(g, &pa0);
             issue_safe(g, &pa1);
         }
@@ -871,7 +879,7 @@ void ovec_step(OVec *v, const int64_t *actions, const int32_t *src, double *rewa
         if (gameover || v->env_steps[gi] >= v->max_steps) {
             gs_load(g, &v->maps[v->game_map[gi]]);
             v->env_steps[gi] = 0;
-            v->aam[gi].n = 0;
+            v->aam[2 * gi].n = v->aam[2 * gi + 1].n = 0;
             for (int k = 0; k < nv; k++) done[6 * (e0 + k)] = 1;
         }
         game_obs(v, gi);

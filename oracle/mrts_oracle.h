@@ -50,7 +50,7 @@ enum { OAI_PASSIVE = 0, OAI_WORKER_RUSH = 1, OAI_LIGHT_RUSH = 2, OAI_RANDOM_BIAS
 
 OVec *ovec_create(int num_selfplay, int num_bot, int max_steps, int partial_obs,
                   const OMap *maps, int num_maps, const int32_t *game_map,
-                  const int32_t *bot_ai);
+                  const int32_t *bot_ai, const int32_t *bot_ai0 /* NULL or -1: agent is p0 */);
 void ovec_destroy(OVec *v);
 int ovec_num_envs(const OVec *v);
 

@@ -501,6 +501,8 @@ static void rush_get_action(const OView *v, OAAMap *m, int army, int po, int coa
 
 /* ---- RandomBiasedAI.getAction --------------------------------------------- */
 static void random_biased_get_action(const OView *v, int game, uint32_t tick, OPA *pa) {
+    /* stream per (unit, tick, game, player); player 1 keeps the 'RAND' tag */
+    const uint32_t tag = 0x52414E44u + (uint32_t)(1 - v->player);
     const OGS *g = v->g;
     const int p = v->player;
     pa_init(pa);
@@ -519,7 +521,7 @@ static void random_biased_get_action(const OView *v, int game, uint32_t tick, OP
         int total = 0;
         for (int k = 0; k < n; k++)
             total += (l[k].type == A_ATTACK || l[k].type == A_HARVEST || l[k].type == A_RETURN) ? 5 : 1;
-        uint32_t ctr[4] = {(uint32_t)i, tick, (uint32_t)game, 0x52414E44u};
+        uint32_t ctr[4] = {(uint32_t)i, tick, (uint32_t)game, tag};
         philox(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
         int t = (int)(((uint64_t)ctr[0] * (uint32_t)total) >> 32), pick = n - 1;
         for (int k = 0; k < n; k++) {
@@ -540,10 +542,10 @@ static void random_biased_get_action(const OView *v, int game, uint32_t tick, OP
     }
 }
 
-/* ai2.getAction(1, gs) for a bot game */
-static void bot_get_action(const OGS *g, int ai, int partial, int game, uint32_t tick, OAAMap *m, OPA *pa) {
+/* ai.getAction(player, gs) for a bot game: ai2 for player 1 (bot envs), and
+ * ai1 for player 0 in bot-vs-bot games (MicroRTSBotVecEnv, vec_env.py:1104-1236) */
+static void bot_get_action(const OGS *g, int ai, int player, int partial, int game, uint32_t tick, OAAMap *m, OPA *pa) {
     uint8_t *hidden = NULL;
-    const int player = 1;
     if (partial) {
         hidden = (uint8_t *)calloc(g->nu + 1, 1);
         for (int i = 0; i < g->nu; i++)

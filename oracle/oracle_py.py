@@ -36,7 +36,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         L.ovec_create.restype = P
-        L.ovec_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P]
+        L.ovec_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P, P]
         L.ovec_destroy.argtypes = [P]
         L.ovec_reset.argtypes = [P]
         L.ovec_reset_game.argtypes = [P, ctypes.c_int, ctypes.c_int]
@@ -88,7 +88,7 @@ class OracleVecEnv:
     """The oracle behind a MicroRTSGridModeVecEnv-shaped surface."""
 
     def __init__(self, num_selfplay_envs, num_bot_envs, map_paths, max_steps=2000, partial_obs=False,
-                 ai2s=None, reward_weight=None, game_maps=None):
+                 ai2s=None, reward_weight=None, game_maps=None, ai1s=None):
         self.num_selfplay_envs, self.num_bot_envs = num_selfplay_envs, num_bot_envs
         self.num_envs = num_selfplay_envs + num_bot_envs
         self.num_games = num_selfplay_envs // 2 + num_bot_envs
@@ -107,8 +107,12 @@ class OracleVecEnv:
         ai = np.array([AI_IDS[a] if isinstance(a, str) else a for a in (ai2s or [0] * num_bot_envs)], np.int32)
         if ai.size == 0:
             ai = np.zeros(1, np.int32)
+        # bot-vs-bot games (MicroRTSBotVecEnv): ai1s[j] plays player 0 of bot env j
+        ai0 = np.array([AI_IDS[a] if isinstance(a, str) else a for a in ai1s], np.int32) if ai1s else None
+        self._ai0 = ai0
         self._h = lib().ovec_create(num_selfplay_envs, num_bot_envs, max_steps, int(partial_obs),
-                                    ctypes.cast(arr, ctypes.c_void_p), len(self.maps), ptr(gm), ptr(ai))
+                                    ctypes.cast(arr, ctypes.c_void_p), len(self.maps), ptr(gm), ptr(ai),
+                                    ptr(ai0) if ai0 is not None else None)
         self.reward_weight = np.asarray(reward_weight if reward_weight is not None else [10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
         hw = self.height * self.width
         self.P_raw = 7 if partial_obs else 6

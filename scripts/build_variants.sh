@@ -9,9 +9,6 @@ S="$C/mrts_engine.hip $C/mrts_bots.hip $C/mrts_capi.cpp"
 build() { name=$1; shift; /opt/rocm/bin/hipcc $F "$@" -o scripts/_exp/lib_$name.so $S & }
 build base
 build noobs -DMRTS_EXP_NOOBS
-build stop1 -DMRTS_EXP_STOP=1
-build stop2 -DMRTS_EXP_STOP=2
-build stop3 -DMRTS_EXP_STOP=3
-build stop4 -DMRTS_EXP_STOP=4
+build s_b4 -DMRTS_SAMPLE_BLOCKS_PER_CU=4
 wait
 ls -la scripts/_exp

@@ -88,3 +88,26 @@ def test_random_biased_acts():
     # the bot's units do something: action planes other than NONE appear for enemy units
     acting = sum(int(((o[..., 12] == 1) & (o[..., 21] == 0)).sum()) for o in r["obs"])
     assert acting > 0
+
+
+def test_bot_vs_bot_outcomes_league_reference():
+    """MicroRTSBotVecEnv games of the restated bots on basesWorkers16x16A
+    (league.py:192, 236-245 setting, max_steps 5000).  league.db
+    records coacAI (p0) beating randomBiasedAI and passiveAI 5/5 -- reproduced
+    here.  Its coacAI-vs-workerRush / vs-lightRush outcomes are NOT reproduced by
+    the restated coacAI: outcome-level parity is partial."""
+    m = os.path.join(MAPS, "maps/16x16/basesWorkers16x16A.xml")
+    for a2 in ["randomBiasedAI", "passiveAI"]:
+        n = 5
+        e = OracleVecEnv(0, n, [m], max_steps=5000, ai2s=[a2] * n, ai1s=["coacAI"] * n)
+        e.reset()
+        res = [None] * n
+        for s in range(5000):
+            e.source_unit_mask = np.zeros((n, 256), np.int32)
+            r, d = e.step_raw(np.zeros((n, 256, 7), np.int64))
+            for k in np.nonzero(d[:, 0])[0]:
+                if res[k] is None:
+                    res[k] = int(r[k, 0])
+            if all(x is not None for x in res):
+                break
+        assert res == [1] * n, (a2, res)

@@ -81,3 +81,37 @@ def test_bots_adversarial_agent_actions():
 
 def test_bots_tensor_path_and_long_episodes():
     lockstep(BOTS * 2, "maps/16x16/basesWorkers16x16.xml", 0, 2100, return_tensors=True, partial_obs=True)
+
+
+@pytest.mark.parametrize("partial_obs", [False, True])
+def test_bot_vs_bot_env_matches_oracle(partial_obs):
+    """MicroRTSBotVecEnv (vec_env.py:1104-1236): both players are device bots."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSBotVecEnv
+    from oracle_py import OracleVecEnv
+
+    ai1 = (BOTS * 2)[:12]
+    ai2 = list(reversed(ai1))
+    m = "maps/16x16/basesWorkers16x16A.xml"
+    w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    g = MicroRTSBotVecEnv(ai1s=[getattr(microrts_ai, a) for a in ai1], ai2s=[getattr(microrts_ai, a) for a in ai2],
+                          map_paths=[m], max_steps=700, partial_obs=partial_obs, reward_weight=w)
+    o = OracleVecEnv(0, len(ai1), [os.path.join(MAPS, m)], max_steps=700, ai2s=ai2, ai1s=ai1, partial_obs=partial_obs,
+                     reward_weight=w)
+    assert g.reset().shape == (12, 2)
+    o.reset()
+    hw = g.height * g.width
+    finished = 0
+    for s in range(1500):
+        _, rg, dg, ig = g.step(np.zeros((12, hw * 7), np.int64))
+        o.source_unit_mask = np.zeros((12, hw), np.int32)
+        ro, do = o.step_raw(np.zeros((12, hw, 7), np.int64))
+        np.testing.assert_array_equal(np.array([i["raw_rewards"] for i in ig]), ro, err_msg=f"step {s}")
+        np.testing.assert_array_equal(dg, do[:, 0])
+        np.testing.assert_array_equal(rg, ro @ w)
+        np.testing.assert_array_equal(g._obs.cpu().numpy().astype(np.int32), o.encode(o.raw_obs()), err_msg=f"obs {s}")
+        finished += int(do[:, 0].sum())
+    assert finished > 12
+    assert g.error_flags() == 0
