@@ -56,7 +56,53 @@ WORKLOADS = {
     "partial_obs": (MAP, "all", 0, None, True),       # configs[3]: partial_obs=True, 31 planes
     "8x8": ("maps/8x8/basesWorkers8x8.xml", "all", 0, None, False),
     "24x24": ("maps/24x24/basesWorkers24x24.xml", "all", 0, None, False),
+    "mixed": (None, None, None, None, False),           # configs[4]: 8x8 / 16x16 / 24x24 buckets, bots + selfplay
 }
+
+# configs[4]: mixed sizes bucketed in one batch; per bucket (map, selfplay envs, bot envs per bot kind)
+MIXED = [("maps/8x8/basesWorkers8x8.xml", 0.25), ("maps/16x16/basesWorkers16x16.xml", 0.5),
+         ("maps/24x24/basesWorkers24x24.xml", 0.25)]
+
+
+def run_mixed(args, rank, dev):
+    """BASELINE configs[4]: one MicroRTSMixedMapVecEnv with an 8x8, a 16x16 and a 24x24
+    bucket, each half selfplay envs, a quarter vs device workerRushAI, a quarter vs
+    device coacAI; envs_per_gpu split 1:2:1 over the buckets."""
+    import numpy as np
+    import torch
+
+    from gym_microrts import _native, microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
+
+    n = args.envs_per_gpu
+    buckets = []
+    for m, frac in MIXED:
+        nb = int(n * frac) // 4 * 4
+        bots = [microrts_ai.workerRushAI] * (nb // 4) + [microrts_ai.coacAI] * (nb // 4)
+        buckets.append(dict(map_paths=[m], num_selfplay_envs=nb // 2, num_bot_envs=len(bots), ai2s=bots))
+    env = MicroRTSMixedMapVecEnv(buckets, max_steps=args.max_steps, device=dev, return_tensors=True,
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]))
+    lib = _native.lib()
+    acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=dev) for e in env.envs]
+    seed = (args.seed << 32) | rank
+
+    def one_step(s):
+        masks = env.get_action_mask()
+        for e, m, a in zip(env.envs, masks, acts):
+            _native.check(lib.mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), e.num_envs,
+                                                  e.height * e.width, seed, s, a.data_ptr()), None, "sample")
+        return env.step(acts)
+
+    env.reset()
+    for s in range(args.warmup):
+        one_step(s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, args.warmup + args.steps):
+        one_step(s)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    return elapsed, {}, env.error_flags(), 256, sum(e.num_envs for e in env.envs) // 2, env.num_envs, 29
 
 
 WORKLOAD_DESC = {
@@ -66,6 +112,8 @@ WORKLOAD_DESC = {
     "partial_obs": "16x16 basesWorkers selfplay, partial_obs=True (31 planes), random masked actions",
     "8x8": "8x8 basesWorkers selfplay, random masked actions",
     "24x24": "24x24 basesWorkers selfplay, random masked actions",
+    "mixed": "8x8 / 16x16 / 24x24 basesWorkers buckets (1:2:1) in one batch, each half selfplay, a quarter vs "
+             "device workerRushAI, a quarter vs device coacAI; random masked agent actions",
 }
 
 
@@ -226,7 +274,11 @@ def main():
 
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    elapsed, kern, flags, hw, G, N, P = run_gpu(args, rank, world, local_rank)
+    if args.workload == "mixed":
+        torch.cuda.set_device(local_rank)
+        elapsed, kern, flags, hw, G, N, P = run_mixed(args, rank, torch.device("cuda", local_rank))
+    else:
+        elapsed, kern, flags, hw, G, N, P = run_gpu(args, rank, world, local_rank)
     dev = torch.device("cuda", local_rank)
     elapsed_max = max_over_ranks(elapsed, world, dev)
     total_env_steps = world * N * args.steps

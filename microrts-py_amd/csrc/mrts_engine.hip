@@ -889,15 +889,14 @@ __device__ __forceinline__ void sample_load(SampleBuf& B, const int32_t* __restr
     const int rb = (int)min((long long)SW, rows - row0);
     const int nv = rb * MRTS_MASK_CH / 4;
     const int4* m4 = reinterpret_cast<const int4*>(mask + row0 * MRTS_MASK_CH);
+    // Unconditional loads (tail lanes re-read the group's last int4 and are
+    // masked when consumed): no branch around a load, so hipcc can count them and
+    // wait with vmcnt(SNV) for this group while the next one stays in flight.
 #pragma unroll
     for (int j = 0; j < SNV; j++) {
-        const int k = j * 64 + (threadIdx.x & 63);
-        if (k < nv) {   // streamed once: non-temporal (no L2 allocation)
-            const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(m4 + k));
-            B.v[j] = make_int4(t.x, t.y, t.z, t.w);
-        } else {
-            B.v[j] = make_int4(0, 0, 0, 0);
-        }
+        const int k = min(j * 64 + (int)(threadIdx.x & 63), nv - 1);
+        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(m4 + k));   // streamed once
+        B.v[j] = make_int4(t.x, t.y, t.z, t.w);
     }
 }
 
@@ -990,12 +989,12 @@ __global__ __launch_bounds__(64 * SWAVES, MRTS_SAMPLE_MIN_WAVES) void k_sample(c
     SampleBuf A, B;
     sample_load(A, mask, grp, rows);
     while (true) {   // two groups per trip: A is consumed while B loads, then the reverse
-        const long long g1 = grp + stride;
-        if (g1 < ngrp) sample_load(B, mask, g1, rows);
+        const long long g1 = grp + stride;   // past the end: a harmless re-read of the last group
+        sample_load(B, mask, min(g1, ngrp - 1), rows);
         sample_group(A, mask, grp, rows, hw, seed, step, act, s_bits[w], s_out[w]);
         if (g1 >= ngrp) break;
         const long long g2 = g1 + stride;
-        if (g2 < ngrp) sample_load(A, mask, g2, rows);
+        sample_load(A, mask, min(g2, ngrp - 1), rows);
         sample_group(B, mask, g1, rows, hw, seed, step, act, s_bits[w], s_out[w]);
         if (g2 >= ngrp) break;
         grp = g2;

@@ -434,3 +434,61 @@ class MicroRTSBotVecEnv(MicroRTSGridModeVecEnv):
         done = self._done.cpu().numpy().astype(bool)
         infos = [{"raw_rewards": item} for item in reward]
         return np.ones((self.num_envs, 2)), reward @ self.reward_weight, done[:, 0], infos
+
+
+class MicroRTSMixedMapVecEnv:
+    """Maps of several sizes in one batch (BASELINE.json config 5), bucketed by
+    height x width: one MicroRTSGridModeVecEnv engine per bucket, all launched on
+    the caller's HIP stream back to back.  The reference's vec env requires one
+    map size per env (vec_env.py:148-150), so each bucket keeps the reference's
+    exact shapes and contract; the mixed env returns one entry per bucket.
+
+      buckets = [dict(map_paths=[...], num_selfplay_envs=..., num_bot_envs=..., ai2s=[...]), ...]
+      env = MicroRTSMixedMapVecEnv(buckets, max_steps=2000, return_tensors=True)
+      obs  = env.reset()                       # list over buckets
+      mask = env.get_action_mask()             # list over buckets
+      obs, rew, done, infos = env.step(actions)  # actions: list over buckets
+    """
+
+    def __init__(self, buckets, **common):
+        self.envs = []
+        for b in buckets:
+            kw = dict(common)
+            kw.update(b)
+            kw.setdefault("num_bot_envs", len(kw.get("ai2s", [])))
+            kw.setdefault("num_selfplay_envs", 0)
+            self.envs.append(MicroRTSGridModeVecEnv(**kw))
+        sizes = [(e.height, e.width) for e in self.envs]
+        if len(set(sizes)) != len(sizes):
+            raise ValueError(f"one bucket per map size, got {sizes}")
+        self.num_envs = sum(e.num_envs for e in self.envs)
+        self.shapes = sizes
+
+    def reset(self):
+        return [e.reset() for e in self.envs]
+
+    def get_action_mask(self):
+        return [e.get_action_mask() for e in self.envs]
+
+    def step_async(self, actions):
+        assert len(actions) == len(self.envs)
+        for e, a in zip(self.envs, actions):
+            e.step_async(a)
+
+    def step_wait(self):
+        outs = [e.step_wait() for e in self.envs]
+        return tuple(list(x) for x in zip(*outs))
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def error_flags(self):
+        f = 0
+        for e in self.envs:
+            f |= e.error_flags()
+        return f
+
+    def close(self):
+        for e in self.envs:
+            e.close()

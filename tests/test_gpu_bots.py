@@ -115,3 +115,38 @@ def test_bot_vs_bot_env_matches_oracle(partial_obs):
         finished += int(do[:, 0].sum())
     assert finished > 12
     assert g.error_flags() == 0
+
+
+def test_mixed_map_buckets_match_oracle():
+    """BASELINE configs[4]: 8x8 / 16x16 / 24x24 buckets in one MicroRTSMixedMapVecEnv,
+    selfplay + device workerRush / coacAI envs, every bucket bit-exact vs its oracle."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
+    from oracle_py import OracleVecEnv, sample_actions
+
+    spec = [("maps/8x8/basesWorkers8x8.xml", 8, ["workerRushAI", "coacAI"] * 2),
+            ("maps/16x16/basesWorkers16x16.xml", 16, ["coacAI", "workerRushAI", "randomBiasedAI", "lightRushAI"] * 2),
+            ("maps/24x24/basesWorkers24x24.xml", 4, ["workerRushAI", "coacAI"])]
+    w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    env = MicroRTSMixedMapVecEnv([dict(map_paths=[m], num_selfplay_envs=nsp, ai2s=[getattr(microrts_ai, a) for a in ais])
+                                  for m, nsp, ais in spec], max_steps=300, return_tensors=True, reward_weight=w,
+                                 obs_dtype=torch.int32)
+    orc = [OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, m)], max_steps=300, ai2s=ais, reward_weight=w)
+           for m, nsp, ais in spec]
+    for og, oo in zip(env.reset(), [o.reset() for o in orc]):
+        np.testing.assert_array_equal(og.cpu().numpy(), oo)
+    for s in range(400):
+        masks = env.get_action_mask()
+        acts = []
+        for mg, o in zip(masks, orc):
+            mo = o.get_action_mask()
+            np.testing.assert_array_equal(mg.cpu().numpy(), mo)
+            acts.append(sample_actions(mo, 13, s))
+        obs, rew, done, infos = env.step([torch.from_numpy(a).cuda() for a in acts])
+        for k, o in enumerate(orc):
+            oo, ro, do, _ = o.step(acts[k])
+            np.testing.assert_array_equal(obs[k].cpu().numpy(), oo, err_msg=f"bucket {k} step {s}")
+            np.testing.assert_array_equal(done[k].cpu().numpy(), do)
+    assert env.error_flags() == 0
