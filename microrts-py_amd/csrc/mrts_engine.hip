@@ -874,7 +874,10 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
 // selection arithmetic.  The 7 int64 components per row are staged in LDS and
 // written back with coalesced 16-byte stores.  No block barriers: a wave's own
 // LDS operations complete in order.
-constexpr int SW = 32;                                   // rows per group (one wave)
+#ifndef MRTS_SAMPLE_ROWS
+#define MRTS_SAMPLE_ROWS 32
+#endif
+constexpr int SW = MRTS_SAMPLE_ROWS;                     // rows per group (one wave)
 constexpr int SWAVES = 4;                                // waves per workgroup
 constexpr int SNV = (SW * MRTS_MASK_CH / 4 + 63) / 64;   // dwordx4 loads per lane per group (10)
 
@@ -974,7 +977,7 @@ __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* 
 #define MRTS_SAMPLE_MIN_WAVES 1
 #endif
 #ifndef MRTS_SAMPLE_BLOCKS_PER_CU
-#define MRTS_SAMPLE_BLOCKS_PER_CU 2
+#define MRTS_SAMPLE_BLOCKS_PER_CU 16   // measured best (scripts/kernel_variants.py: 2 -> 151 us, 4 -> 138, 8 -> 133, 16 -> 127, 64 -> 178)
 #endif
 __global__ __launch_bounds__(64 * SWAVES, MRTS_SAMPLE_MIN_WAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
                                                         uint32_t step, int64_t* __restrict__ act) {
