@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
+    ap.add_argument("--no-eager-masks", action="store_true",
+                    help="get_action_mask() launches k_masks instead of k_step writing the next tick's masks")
+    ap.add_argument("--sampler", default="src", choices=["src", "dense"],
+                    help="src: mrts_sample_actions_src (reads the mask rows of source cells only); dense: every row")
     ap.add_argument("--workload", default="selfplay", choices=sorted(WORKLOADS),
                     help="selfplay = the BASELINE metric; the others are the secondary BASELINE.json configs")
     return ap.parse_args()
@@ -81,7 +85,7 @@ def run_mixed(args, rank, dev):
         bots = [microrts_ai.workerRushAI] * (nb // 4) + [microrts_ai.coacAI] * (nb // 4)
         buckets.append(dict(map_paths=[m], num_selfplay_envs=nb // 2, num_bot_envs=len(bots), ai2s=bots))
     env = MicroRTSMixedMapVecEnv(buckets, max_steps=args.max_steps, device=dev, return_tensors=True,
-                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]))
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), eager_masks=not args.no_eager_masks)
     lib = _native.lib()
     acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=dev) for e in env.envs]
     seed = (args.seed << 32) | rank
@@ -89,8 +93,7 @@ def run_mixed(args, rank, dev):
     def one_step(s):
         masks = env.get_action_mask()
         for e, m, a in zip(env.envs, masks, acts):
-            _native.check(lib.mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), e.num_envs,
-                                                  e.height * e.width, seed, s, a.data_ptr()), None, "sample")
+            _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, seed, s, a), None, "sample")
         return env.step(acts)
 
     env.reset()
@@ -102,7 +105,7 @@ def run_mixed(args, rank, dev):
         one_step(s)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    return elapsed, {}, env.error_flags(), 256, sum(e.num_envs for e in env.envs) // 2, env.num_envs, 29
+    return elapsed, {}, env.error_flags(), 256, sum(e.num_envs for e in env.envs) // 2, env.num_envs, 29, 0
 
 
 WORKLOAD_DESC = {
@@ -117,6 +120,17 @@ WORKLOAD_DESC = {
 }
 
 
+def sample(lib, kind, mask, source, n, hw, seed, step, act):
+    """The bench's stand-in policy: a uniform pick among the valid entries of
+    every component of every cell (hello_world.py:27-64), on the device."""
+    import torch
+
+    st = torch.cuda.current_stream().cuda_stream
+    if kind == "src":
+        return lib.mrts_sample_actions_src(st, mask.data_ptr(), source.data_ptr(), n, hw, seed, step, act.data_ptr())
+    return lib.mrts_sample_actions(st, mask.data_ptr(), n, hw, seed, step, act.data_ptr())
+
+
 def shard(rank, n):
     """rank r owns global envs [r*n, (r+1)*n); n even so selfplay pairs never straddle
     ranks; the sampler seed is shard-specific."""
@@ -124,16 +138,21 @@ def shard(rank, n):
     return rank * n, (rank + 1) * n
 
 
-def kernel_bytes(G, N, HW, P=29):
+def kernel_bytes(G, N, HW, P=29, eager=True, sampler="src", src_rows=0):
     """Algorithmic bytes per launch.
     masks: game state read (16 B/cell/game) + mask write (78*4 B/cell/env) + source write (4 B/cell/env).
     step : game state read+write (32 B/cell/game) + source read (4 B/cell/env) + obs write (4P B/cell/env)
-           + raw reward (48 B/env) + done (6 B/env); action rows (56 B per acting unit) not counted."""
-    return {
-        "get_masks": G * HW * 16 + N * HW * (78 * 4 + 4),
-        "step": G * HW * 32 + N * HW * (4 + 4 * P) + N * (48 + 6 + 8 + 1),
-        "sample": N * HW * (78 * 4 + 7 * 8),
-    }
+           + raw reward (48 B/env) + done (6 B/env) + fused reward / done0 (9 B/env); action rows (56 B
+           per acting unit) not counted.  Eager masks: + the next tick's mask and source writes.
+    sample: dense -- every mask row read + actions written; src -- source read, the mask rows of
+           `src_rows` source cells read, actions written."""
+    masks = N * HW * (78 * 4 + 4)
+    step = G * HW * 32 + N * HW * (4 + 4 * P) + N * (48 + 6 + 8 + 1) + (masks if eager else 0)
+    if sampler == "dense":
+        samp = N * HW * (78 * 4 + 7 * 8)
+    else:
+        samp = N * HW * (4 + 7 * 8) + src_rows * 78 * 4
+    return {"get_masks": G * HW * 16 + masks, "step": step, "sample": samp}
 
 
 # rocprofv3 kernel names -> bench kernel names
@@ -172,7 +191,8 @@ def run_gpu(args, rank, world, local_rank):
     nbot = n if nbot == "all" else nbot
     env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
                                  ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
-                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, return_tensors=True)
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, return_tensors=True,
+                                 eager_masks=not args.no_eager_masks)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
     lib = _native.lib()
@@ -185,7 +205,7 @@ def run_gpu(args, rank, world, local_rank):
         if env.kernel_events is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        rc = lib.mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), n, hw, seed, s, act.data_ptr())
+        rc = sample(lib, args.sampler, m, env.source_unit_mask, n, hw, seed, s, act)
         if env.kernel_events is not None:
             e1.record()
             env.kernel_events.setdefault("sample", []).append((e0, e1))
@@ -209,7 +229,8 @@ def run_gpu(args, rank, world, local_rank):
     flags = env.error_flags()
     kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
     G = nsp // 2 + nbot
-    return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes)
+    src_rows = int(env.source_unit_mask.sum().item())   # source cells of the last step (sampler bytes)
+    return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes), src_rows
 
 
 def barrier(world, dev):
@@ -276,16 +297,17 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     if args.workload == "mixed":
         torch.cuda.set_device(local_rank)
-        elapsed, kern, flags, hw, G, N, P = run_mixed(args, rank, torch.device("cuda", local_rank))
+        elapsed, kern, flags, hw, G, N, P, src_rows = run_mixed(args, rank, torch.device("cuda", local_rank))
     else:
-        elapsed, kern, flags, hw, G, N, P = run_gpu(args, rank, world, local_rank)
+        elapsed, kern, flags, hw, G, N, P, src_rows = run_gpu(args, rank, world, local_rank)
     dev = torch.device("cuda", local_rank)
     elapsed_max = max_over_ranks(elapsed, world, dev)
     total_env_steps = world * N * args.steps
     value = total_env_steps / elapsed_max
     out = None
     if rank == 0:
-        kb = kernel_bytes(G, N, hw, P)
+        eager = not args.no_eager_masks
+        kb = kernel_bytes(G, N, hw, P, eager=eager, sampler=args.sampler, src_rows=src_rows)
         roof = None
         kernels = {}
         for k, ms in kern.items():
@@ -319,7 +341,10 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOAD_DESC[args.workload],
                        "envs_per_gpu": N, "games_per_gpu": G, "map": WORKLOADS[args.workload][0], "max_steps": args.max_steps,
-                       "obs": f"float32 device tensor, {P} planes", "parallelism": f"env-shard x{world}"},
+                       "obs": f"float32 device tensor, {P} planes", "parallelism": f"env-shard x{world}",
+                       "masks": "next-tick masks written by k_step (eager)" if eager else "k_masks per get_action_mask()",
+                       "sampler": {"src": "mrts_sample_actions_src (mask rows of source cells)",
+                                   "dense": "mrts_sample_actions (every mask row)"}[args.sampler]},
             "roofline": roof,
             "kernels": kernels,
             "env_step_bytes": env_step_bytes,

@@ -96,6 +96,16 @@ int mrts_reset(mrts_vec *h, void *stream, void *obs);
  * (channels 1..78) and source [N][H*W] int32 (channel 0). */
 int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source);
 
+/* Bind device mask outputs (the zero-copy form of the reference's shared-memory
+ * client, Client(..., obsBuf, maskBuf, actionBuf, 0), vec_env.py:1276-1283,
+ * 1310-1324): from now on mrts_reset, mrts_step, mrts_step_weighted and
+ * mrts_reset_games also write getMasks(0) of the state they leave behind --
+ * the bytes a following mrts_get_masks would write -- into mask [N][H*W][78]
+ * int32 and source [N][H*W] int32, in the same kernel pass.  `source` may be
+ * the buffer mrts_step reads its rows from (each game reads its own rows
+ * before it rewrites them).  NULL, NULL unbinds. */
+int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source);
+
 /* step_async + JNIGridnetVecClient.gameStep (vec_env.py:968-984, 1002):
  * actions [N][H*W][7] int64 (device), source [N][H*W] int32 = the source
  * channel of the last mrts_get_masks (selects the rows, vec_env.py:974).
@@ -131,6 +141,12 @@ int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int3
  * (Philox4x32-10 keyed by seed, counter = (cell, env, step)). */
 int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int32_t hw, uint64_t seed,
                         uint32_t step, int64_t *actions);
+
+/* Same stream and output as mrts_sample_actions, given the source channel too:
+ * mask rows of cells whose source is 0 are all zero (getMasks), so only the
+ * rows of source cells are read.  Every row's 7 components are still written. */
+int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t num_envs, int32_t hw,
+                            uint64_t seed, uint32_t step, int64_t *actions);
 
 /* Engine invariant violations recorded on the device (OR over games). */
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out);

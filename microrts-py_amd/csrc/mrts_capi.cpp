@@ -167,6 +167,7 @@ struct mrts_vec {
     std::string err, utt;
     double rw[6] = {0, 0, 0, 0, 0, 0};
     int shaping = 1;
+    int32_t *next_mask = nullptr, *next_src = nullptr;   // mrts_bind_mask_outputs
     EngineParams base{};
 };
 
@@ -329,6 +330,8 @@ int mrts_reset(mrts_vec *h, void *stream, void *obs) {
     if (!bound(h) || !obs) return fail(h, MRTS_ESTATE, "reset: workspace not bound or obs null");
     EngineParams p = h->base;
     p.obs = obs;
+    p.mask = h->next_mask;
+    p.src_out = h->next_src;
     hipError_t e = mrts_engine_reset(&p, (hipStream_t)stream, nullptr, nullptr, 0);
     return e ? hip_fail(h, e, "reset launch") : MRTS_OK;
 }
@@ -352,6 +355,8 @@ int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *
     p.obs = obs;
     p.raw_reward = raw_reward;
     p.done = done;
+    p.mask = h->next_mask;
+    p.src_out = h->next_src;
     hipError_t e = mrts_engine_bots(&p, (hipStream_t)stream);
     if (!e) e = mrts_engine_step(&p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
@@ -384,6 +389,8 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
     p.done0 = done0;
     for (int k = 0; k < 6; k++) p.rw[k] = h->rw[k];
     p.shaping = h->shaping;
+    p.mask = h->next_mask;
+    p.src_out = h->next_src;
     hipError_t e = mrts_engine_bots(&p, (hipStream_t)stream);
     if (!e) e = mrts_engine_step(&p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
@@ -406,6 +413,8 @@ int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int3
     if (e) return hip_fail(h, e, "reset_games upload");
     EngineParams p = h->base;
     p.obs = obs;
+    p.mask = h->next_mask;
+    p.src_out = h->next_src;
     e = mrts_engine_reset(&p, s, dg, dg + count, count);
     if (e) return hip_fail(h, e, "reset_games launch");
     // the host staging vector must outlive the copy
@@ -417,6 +426,21 @@ int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw
                         int64_t *actions) {
     if (!mask || !actions || n < 0 || hw <= 0) return MRTS_EINVAL;
     return mrts_engine_sample(mask, n, hw, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
+}
+
+int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t n, int32_t hw, uint64_t seed,
+                            uint32_t step, int64_t *actions) {
+    if (!mask || !source || !actions || n < 0 || hw <= 0) return MRTS_EINVAL;
+    return mrts_engine_sample_src(mask, source, n, hw, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
+}
+
+int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source) {
+    if (!bound(h)) return fail(h, MRTS_ESTATE, "bind_mask_outputs: workspace not bound");
+    if ((mask == nullptr) != (source == nullptr)) return fail(h, MRTS_EINVAL, "bind_mask_outputs: mask and source go together");
+    if (mask && ((uintptr_t)mask & 15u)) return fail(h, MRTS_EINVAL, "bind_mask_outputs: mask must be 16-byte aligned");
+    h->next_mask = mask;
+    h->next_src = source;
+    return MRTS_OK;
 }
 
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {

@@ -18,8 +18,8 @@ struct EngineParams {
     void *obs;              // [N][HW][P]
     double *raw_reward;     // [N][6]
     uint8_t *done;          // [N][6]
-    int32_t *mask;          // [N][HW][78]
-    int32_t *src_out;       // [N][HW]
+    int32_t *mask;          // [N][HW][78]: k_masks output; k_step / k_reset write the
+    int32_t *src_out;       // [N][HW]      next tick's masks here when non-null
     // optional fused step_wait outputs (vec_env.py:1057): reward = raw @ rw
     // (float64, k = 0..5 in order; channels 1..5 zeroed when !shaping) and done[:,0]
     double *reward;         // [N] or null
@@ -41,6 +41,8 @@ hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_bots(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *raw);
 hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
+hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n, int hw, uint64_t seed, uint32_t step, int64_t *act,
+                                  hipStream_t s);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);
 }

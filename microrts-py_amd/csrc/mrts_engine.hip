@@ -100,7 +100,7 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
 
 // Ordered block-wide compaction: list <- cells c (ascending) with pred(c).
 template <int NT, typename F>
-__device__ int compact_cells(int HW, F pred, int32_t* list, unsigned long long* s_mask) {
+__device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsigned long long* s_mask) {
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int J = (HW + NT - 1) / NT;
@@ -141,7 +141,7 @@ __device__ __forceinline__ Game game_of(const EngineParams& p, int g) {
 
 // PhysicalGameState.load + new GameState into LDS
 template <int NT>
-__device__ void reset_into_lds(const EngineParams& p, const Lds& L, int map) {
+__device__ __forceinline__ void reset_into_lds(const EngineParams& p, const Lds& L, int map) {
     const int HW = p.HW;
     for (int c = threadIdx.x; c < HW; c += NT) {
         int4 v = p.map_cells[(size_t)map * HW + c];
@@ -163,7 +163,7 @@ __device__ void reset_into_lds(const EngineParams& p, const Lds& L, int map) {
 }
 
 template <int NT>
-__device__ void load_game(const EngineParams& p, const Lds& L, int g) {
+__device__ __forceinline__ void load_game(const EngineParams& p, const Lds& L, int g) {
     if (threadIdx.x < MRTS_GENV_WORDS) L.sc[threadIdx.x] = p.genv[(size_t)g * MRTS_GENV_WORDS + threadIdx.x];
     __syncthreads();
     const int HW = p.HW, map = L.sc[SC_MAP];
@@ -180,7 +180,7 @@ __device__ void load_game(const EngineParams& p, const Lds& L, int g) {
 }
 
 template <int NT>
-__device__ void store_game(const EngineParams& p, const Lds& L, int g) {
+__device__ __forceinline__ void store_game(const EngineParams& p, const Lds& L, int g) {
     const int HW = p.HW;
     int4* dst = p.cells + (size_t)g * HW;
     for (int c = threadIdx.x; c < HW; c += NT) dst[c] = make_int4((int)L.unit[c], L.uid[c], (int)L.act[c], (int)L.seq[c]);
@@ -192,7 +192,7 @@ __device__ void store_game(const EngineParams& p, const Lds& L, int g) {
 // player q when some unit of q is within its sight radius (d^2 <= r^2).  Each
 // unit lane ORs its sight disk into the player's LDS bitmap.
 template <int NT>
-__device__ void compute_vis(const EngineParams& p, const Lds& L) {
+__device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L) {
     const int HW = p.HW, nw = HW / 32 + 1;
     for (int i = threadIdx.x; i < 2 * nw; i += NT) L.vis[i] = 0;
     __syncthreads();
@@ -217,7 +217,7 @@ __device__ void compute_vis(const EngineParams& p, const Lds& L) {
 }
 
 template <int NT, int P, typename OT>
-__device__ void write_obs(const EngineParams& p, const Lds& L, int env, int player) {
+__device__ __forceinline__ void write_obs(const EngineParams& p, const Lds& L, int env, int player) {
     const int HW = p.HW;
     if (P == 31) {
         const int nw = HW / 32 + 1;
@@ -257,6 +257,9 @@ __device__ void write_obs(const EngineParams& p, const Lds& L, int env, int play
     __syncthreads();
 }
 
+template <int NT>
+__device__ __forceinline__ void write_masks(const EngineParams& p, const Lds& L, const Game& G);
+
 // ---------------------------------------------------------------------------
 // Reset kernel: every game (or the listed ones) back to its map; obs out.
 template <int NT, int P, typename OT>
@@ -273,6 +276,7 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
     Game G = game_of(p, g);
     if (P == 31) compute_vis<NT>(p, L);
     for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
+    if (p.mask) write_masks<NT>(p, L, G);
 }
 
 // ---------------------------------------------------------------------------
@@ -307,15 +311,15 @@ __global__ __launch_bounds__(NT) void k_raw(EngineParams p, int32_t* raw) {
 }
 
 // ---------------------------------------------------------------------------
-// Mask kernel: JNIGridnetVecClient.getMasks(0) -> [N][HW][78] + source [N][HW]
+// JNIGridnetVecClient.getMasks(0) of the game in LDS -> [N][HW][78] + source
+// [N][HW] of every view: per-cell 79-bit words in LDS, then 16-byte stores.
+// Shared by k_masks (a standalone getMasks) and by k_step / k_reset, which
+// write the masks of the state they leave behind when mask outputs are bound
+// (mrts_bind_mask_outputs): the same bytes a following getMasks would write.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Lds L = carve(smem, p.HW, p.W, NT);
-    const int g = blockIdx.x, HW = p.HW;
-    load_game<NT>(p, L, g);
+__device__ __forceinline__ void write_masks(const EngineParams& p, const Lds& L, const Game& G) {
+    const int HW = p.HW;
     Grid gd{p.W, p.H, HW};
-    Game G = game_of(p, g);
     for (int v = 0; v < G.nviews; v++) {
         const int env = G.env0 + v, player = v;
         const int res = player == 0 ? L.sc[SC_RES0] : L.sc[SC_RES1];
@@ -354,6 +358,16 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
     }
 }
 
+// Mask kernel: JNIGridnetVecClient.getMasks(0) -> [N][HW][78] + source [N][HW]
+template <int NT>
+__global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Lds L = carve(smem, p.HW, p.W, NT);
+    const int g = blockIdx.x;
+    load_game<NT>(p, L, g);
+    write_masks<NT>(p, L, game_of(p, g));
+}
+
 // ---------------------------------------------------------------------------
 // Step kernel: JNIGridnetVecClient.gameStep for one game per workgroup.
 enum : uint32_t { CAND = 1u << 31, LEGAL = 1u << 30 };
@@ -370,7 +384,7 @@ __device__ __forceinline__ int res_of(const Lds& L, int player) { return L.sc[SC
 // cells, `vector` = true: the fromVectorAction consistency filter applies and
 // the LinkedHashMap rank is the cell) or a device bot's PlayerAction (already
 // consistent, rank = position in the list).
-__device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd, int q, const int32_t* list, int n,
+__device__ __forceinline__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd, int q, const int32_t* list, int n,
                              bool vector) {
     const int time = L.sc[SC_TIME];
     // --- fromVectorAction: ResourceUsage.consistentWith(pa.ru) ----------------
@@ -488,7 +502,7 @@ __device__ void issue_player(const EngineParams& p, const Lds& L, const Grid& gd
 // (lane 0, issue order) or, for an independent ready set, one lane per action
 // (PAR: resource / error updates are atomic, the produced unit's id is given).
 template <bool PAR = false>
-__device__ void execute_one(const Lds& L, const Grid& gd, int4 s, int produced_uid = -1) {
+__device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s, int produced_uid = -1) {
     const int c = s.x;
     const uint32_t u = (uint32_t)s.y;
     const int code = (int)(s.z);
@@ -848,6 +862,9 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     if (P == 31) compute_vis<NT>(p, L);
     for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
 #endif
+    // (8) getMasks of the next tick (bound mask outputs): every read of this
+    //     game's source rows (phase 1) is behind the barriers above
+    if (p.mask) write_masks<NT>(p, L, G);
 }
 
 // ---------------------------------------------------------------------------
@@ -863,6 +880,37 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
         c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
+    }
+}
+
+// One row (env e, cell c): the 78 mask channels as bits lo (0..63) | hi (64..77);
+// per component k, a uniform pick among the valid entries (uniform over all
+// entries when none is valid), from two Philox4x32-10 blocks of counter
+// (c, e, step, 0|1) -- the oracle's ovec_sample_actions stream.
+__device__ __forceinline__ void sample_row(uint64_t lo, uint64_t hi, int e, int c, uint64_t seed, uint32_t step, int64_t* out) {
+    uint32_t r[8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
+        philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        r[4 * h] = ctr[0]; r[4 * h + 1] = ctr[1]; r[4 * h + 2] = ctr[2]; r[4 * h + 3] = ctr[3];
+    }
+    const int off[7] = {0, 6, 10, 14, 18, 22, 29};
+    const int len[7] = {6, 4, 4, 4, 4, 7, 49};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        uint64_t seg = (lo >> off[k]) | (off[k] ? (hi << (64 - off[k])) : 0);   // bits [off, off+len)
+        seg &= (1ull << len[k]) - 1ull;
+        const int nvalid = __popcll(seg);
+        int pick;
+        if (nvalid == 0) {
+            pick = (int)(((uint64_t)r[k] * (uint32_t)len[k]) >> 32);
+        } else {
+            int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
+            for (; t > 0; t--) seg &= seg - 1ull;   // drop the t lowest set bits
+            pick = __builtin_ctzll(seg);
+        }
+        out[k] = pick;
     }
 }
 
@@ -938,30 +986,7 @@ __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* 
         const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
         const uint64_t lo = (uint64_t)s_bits[3 * lane] | ((uint64_t)s_bits[3 * lane + 1] << 32);
         const uint64_t hi = s_bits[3 * lane + 2];
-        uint32_t r[8];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
-            philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-            r[4 * h] = ctr[0]; r[4 * h + 1] = ctr[1]; r[4 * h + 2] = ctr[2]; r[4 * h + 3] = ctr[3];
-        }
-        const int off[7] = {0, 6, 10, 14, 18, 22, 29};
-        const int len[7] = {6, 4, 4, 4, 4, 7, 49};
-#pragma unroll
-        for (int k = 0; k < 7; k++) {
-            uint64_t seg = (lo >> off[k]) | (off[k] ? (hi << (64 - off[k])) : 0);   // bits [off, off+len)
-            seg &= (1ull << len[k]) - 1ull;
-            const int nvalid = __popcll(seg);
-            int pick;
-            if (nvalid == 0) {
-                pick = (int)(((uint64_t)r[k] * (uint32_t)len[k]) >> 32);
-            } else {
-                int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
-                for (; t > 0; t--) seg &= seg - 1ull;   // drop the t lowest set bits
-                pick = __builtin_ctzll(seg);
-            }
-            s_out[lane * 7 + k] = pick;
-        }
+        sample_row(lo, hi, e, c, seed, step, s_out + lane * 7);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int64_t* ob = act + row0 * 7;   // 16-B aligned: SW * 56 B per group
@@ -1002,6 +1027,62 @@ __global__ __launch_bounds__(64 * SWAVES, MRTS_SAMPLE_MIN_WAVES) void k_sample(c
         if (g2 >= ngrp) break;
         grp = g2;
     }
+}
+
+// Source-guided variant: the same stream and output, given the source channel
+// as well.  getMasks sets no channel of a cell whose source bit is 0 (no idle
+// unit of the player: UnitAction.getValidActionArray is all zero), so only the
+// mask rows of source cells are read -- a few per cent of the 78-channel rows
+// on basesWorkers -- while every row's 7 components are still drawn and
+// written.  One wave per 64 consecutive rows: the wave reads the rows of its
+// active lanes cooperatively (channel k on lane k, two coalesced loads per row,
+// up to four rows in flight) and folds each with two ballots.
+constexpr int SR_WAVES = 4;
+__global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n,
+                                                           int hw, uint64_t seed, uint32_t step, int64_t* __restrict__ act) {
+    __shared__ __attribute__((aligned(16))) int64_t s_out[SR_WAVES][64 * 7];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long rows = (long long)n * hw;
+    const long long row0 = ((long long)blockIdx.x * SR_WAVES + w) * 64;
+    if (row0 >= rows) return;
+    const int rb = (int)min(64ll, rows - row0);
+    const bool in = lane < rb;
+    const int s = in ? src[row0 + lane] : 0;
+    uint64_t pending = __ballot(s != 0);
+    uint64_t lo = 0, hi = 0;   // this lane's row as 78 bits
+    while (pending) {          // wave-uniform
+        int r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            r[k] = pending ? __builtin_ctzll(pending) : r[0];   // repeats r[0]: a harmless duplicate load
+            pending &= pending - 1ull;
+        }
+        int v0[4], v1[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {   // unconditional: all eight loads in flight before the first ballot
+            const int32_t* m = mask + (row0 + r[k]) * MRTS_MASK_CH;
+            v0[k] = __builtin_nontemporal_load(m + lane);
+            v1[k] = __builtin_nontemporal_load(m + 64 + min(lane, MRTS_MASK_CH - 65));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t b0 = __ballot(v0[k] != 0);
+            const uint64_t b1 = __ballot(lane < MRTS_MASK_CH - 64 && v1[k] != 0);
+            if (lane == r[k]) { lo = b0; hi = b1; }
+        }
+    }
+    if (in) {
+        const long long idx = row0 + lane;
+        const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
+        sample_row(lo, hi, e, c, seed, step, s_out[w] + lane * 7);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    int64_t* ob = act + row0 * 7;   // 16-B aligned: 64 * 56 B per wave
+    const int onel = rb * 7, onv = onel >> 1;
+    int4* o4 = reinterpret_cast<int4*>(ob);
+    const int4* s4 = reinterpret_cast<const int4*>(s_out[w]);
+    for (int k = lane; k < onv; k += 64) o4[k] = s4[k];
+    if ((onel & 1) && lane == 0) ob[onel - 1] = s_out[w][onel - 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -1063,6 +1144,14 @@ hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed,
     const long long groups = ((long long)total + mrts::SW - 1) / mrts::SW;
     const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * MRTS_SAMPLE_BLOCKS_PER_CU);   // resident blocks
     hipLaunchKernelGGL(mrts::k_sample, dim3((unsigned)blocks), dim3(64 * mrts::SWAVES), 0, s, mask, n, hw, seed, step, act);
+    return hipGetLastError();
+}
+hipError_t mrts_engine_sample_src(const int32_t* mask, const int32_t* src, int n, int hw, uint64_t seed, uint32_t step, int64_t* act,
+                                  hipStream_t s) {
+    const long long rows = (long long)n * hw;
+    if (rows == 0) return hipSuccess;
+    const long long blocks = (rows + 64 * mrts::SR_WAVES - 1) / (64 * mrts::SR_WAVES);
+    hipLaunchKernelGGL(mrts::k_sample_src, dim3((unsigned)blocks), dim3(64 * mrts::SR_WAVES), 0, s, mask, src, n, hw, seed, step, act);
     return hipGetLastError();
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {

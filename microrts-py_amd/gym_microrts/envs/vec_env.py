@@ -123,6 +123,7 @@ class MicroRTSGridModeVecEnv:
         device=None,
         return_tensors=False,
         obs_dtype=None,
+        eager_masks=True,
         _ai1s=None,
     ):
         # vec_env.py:110-127
@@ -224,6 +225,14 @@ class MicroRTSGridModeVecEnv:
         _native.check(_native.lib().mrts_bind_workspace(self._h, self._ws.data_ptr(), self._stream()), self._h, "bind_workspace")
         rw = np.ascontiguousarray(np.asarray(reward_weight, dtype=np.float64).reshape(6))
         _native.check(_native.lib().mrts_set_reward_weight(self._h, rw.ctypes.data, int(bool(reward_shaping))), self._h, "set_reward_weight")
+        # eager masks: reset / step / map-cycling resets also write getMasks(0) of
+        # the state they leave (mrts_bind_mask_outputs), in the same kernel pass, so
+        # get_action_mask() after them launches nothing (the rollout loop calls it
+        # once per step, ppo_gridnet.py:448-466)
+        self.eager_masks = bool(eager_masks)
+        if self.eager_masks:
+            _native.check(_native.lib().mrts_bind_mask_outputs(self._h, self._mask.data_ptr(), self._src.data_ptr()), self._h,
+                          "bind_mask_outputs")
 
         # computed properties (vec_env.py:230-254)
         self.action_space_dims = [6, 4, 4, 4, 4, len(self.utt["unitTypes"]), 7 * 7]
@@ -236,7 +245,7 @@ class MicroRTSGridModeVecEnv:
         self.action_plane_space = MultiDiscrete(self.action_space_dims)
         self.source_unit_idxs = np.tile(np.arange(self.height * self.width), (self.num_envs, 1))
         self.source_unit_idxs = self.source_unit_idxs.reshape((self.source_unit_idxs.shape + (1,)))
-        self._mask_valid = False
+        self._mask_fresh = False   # _mask / _src hold getMasks(0) of the current state
         # optional {kernel name: [(start, end) torch.cuda.Event]} filled around
         # each engine launch on the launch stream (bench.py roofline timing)
         self.kernel_events = None
@@ -265,13 +274,16 @@ class MicroRTSGridModeVecEnv:
     def reset(self):
         """vec_env.py:278-282"""
         _native.check(_native.lib().mrts_reset(self._h, self._stream(), self._obs.data_ptr()), self._h, "reset")
-        self._mask_valid = False
+        self._mask_fresh = self.eager_masks
         return self._obs_out()
 
     def get_action_mask(self):
-        """vec_env.py:1091-1101: (N, H*W, 78); channel 0 kept as source_unit_mask."""
-        self._launch("get_masks", _native.lib().mrts_get_masks, self._h, self._stream(), self._mask.data_ptr(), self._src.data_ptr())
-        self._mask_valid = True
+        """vec_env.py:1091-1101: (N, H*W, 78); channel 0 kept as source_unit_mask.
+        With eager masks the last reset / step already wrote them."""
+        if not self._mask_fresh:
+            self._launch("get_masks", _native.lib().mrts_get_masks, self._h, self._stream(), self._mask.data_ptr(),
+                         self._src.data_ptr())
+            self._mask_fresh = True
         if self.return_tensors:
             return self._mask
         return self._mask.cpu().numpy()
@@ -296,12 +308,12 @@ class MicroRTSGridModeVecEnv:
 
     def step_wait(self):
         """vec_env.py:1001-1057"""
-        if not self._mask_valid:
+        if not self._mask_fresh:
             # the reference reads the source mask of the last get_action_mask
             # (vec_env.py:974); compute it if the caller skipped that call
             self.get_action_mask()
         a = self._actions_in
-        self._mask_valid = False
+        self._mask_fresh = self.eager_masks
         if self.return_tensors:
             # reward @ reward_weight and done[:, 0] are fused into the step kernel
             self._launch("step", _native.lib().mrts_step_weighted, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
@@ -412,7 +424,7 @@ class MicroRTSBotVecEnv(MicroRTSGridModeVecEnv):
             map_paths = [map_paths]
         super().__init__(num_selfplay_envs=0, num_bot_envs=len(ai1s), partial_obs=partial_obs, max_steps=max_steps,
                          render_theme=render_theme, ai2s=ai2s, map_paths=map_paths, reward_weight=reward_weight,
-                         device=device, _ai1s=ai1s)
+                         device=device, eager_masks=False, _ai1s=ai1s)
         self.ai1s = ai1s
         self.observation_space = Discrete(2)
         self.action_space = Discrete(2)

@@ -66,13 +66,14 @@ def test_kat_reward():
     kat.check_rewards(make_gpu_env)
 
 
-def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_tensors=False, partial_obs=False):
+def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_tensors=False, partial_obs=False,
+             eager_masks=True):
     """Lock-step GPU vs oracle rollout; compares masks, obs, rewards, dones."""
     from oracle_py import sample_actions
 
     torch = _torch()
     g = make_gpu_env(nsp, nbot, map_path, max_steps, return_tensors=return_tensors,
-                     obs_dtype=torch.int32 if return_tensors else None, partial_obs=partial_obs)
+                     obs_dtype=torch.int32 if return_tensors else None, partial_obs=partial_obs, eager_masks=eager_masks)
     o = make_oracle(nsp, nbot, map_path, max_steps, partial_obs=partial_obs)
     og = np.asarray(g.reset().cpu() if return_tensors else g.reset())
     oo = o.reset()
@@ -154,6 +155,88 @@ def test_partial_obs_tensor_path():
 
 def test_tensor_path_bit_exact():
     _rollout("maps/16x16/basesWorkers16x16.xml", 32, 0, 300, 300, seed=3, return_tensors=True)
+
+
+@pytest.mark.parametrize("partial_obs", [False, True])
+def test_standalone_mask_kernel_rollout(partial_obs):
+    """eager_masks=False: every get_action_mask() launches k_masks (the masks
+    are not written by the step kernel)."""
+    _rollout("maps/16x16/basesWorkers16x16.xml", 16, 8, 200, 300, seed=8, partial_obs=partial_obs, eager_masks=False)
+
+
+@pytest.mark.parametrize("map_path", ["maps/16x16/basesWorkers16x16.xml", "maps/24x24/basesWorkers24x24.xml",
+                                      "maps/4x4/baseTwoWorkers4x4.xml"])
+def test_eager_masks_equal_mask_kernel(map_path):
+    """The masks k_step / k_reset write for the next tick are the bytes k_masks
+    writes for the same state (mask and source channel), every step."""
+    import ctypes
+
+    from gym_microrts import _native
+
+    torch = _torch()
+    g = make_gpu_env(16, 8, map_path, 150, return_tensors=True)
+    g.reset()
+    hw = g.height * g.width
+    m2 = torch.full((g.num_envs, hw, 78), -1, dtype=torch.int32, device=g.device)
+    s2 = torch.full((g.num_envs, hw), -1, dtype=torch.int32, device=g.device)
+    act = torch.empty((g.num_envs, hw, 7), dtype=torch.int64, device=g.device)
+    st = torch.cuda.current_stream().cuda_stream
+    for s in range(300):
+        m = g.get_action_mask()
+        _native.check(_native.lib().mrts_get_masks(g._h, st, m2.data_ptr(), s2.data_ptr()), g._h, "get_masks")
+        assert torch.equal(m, m2), f"mask step {s}"
+        assert torch.equal(g.source_unit_mask, s2), f"source step {s}"
+        _native.check(_native.lib().mrts_sample_actions(st, m.data_ptr(), g.num_envs, hw, ctypes.c_uint64(5), s, act.data_ptr()))
+        g.step(act)
+    assert g.error_flags() == 0
+
+
+def test_source_guided_sampler_equals_dense_sampler():
+    """mrts_sample_actions_src reads only the mask rows of source cells; the
+    output is the dense sampler's (and the oracle's) bit for bit."""
+    import ctypes
+
+    from gym_microrts import _native
+    from oracle_py import sample_actions
+
+    torch = _torch()
+    g = make_gpu_env(256, 0, "maps/16x16/basesWorkers16x16.xml", 2000, return_tensors=True)
+    g.reset()
+    st = torch.cuda.current_stream().cuda_stream
+    a1 = torch.empty((256, 256, 7), dtype=torch.int64, device=g.device)
+    a2 = torch.full((256, 256, 7), -1, dtype=torch.int64, device=g.device)
+    for s in range(60):
+        m = g.get_action_mask()
+        seed = ctypes.c_uint64(0x0123456789ABCDEF + s)
+        _native.check(_native.lib().mrts_sample_actions(st, m.data_ptr(), 256, 256, seed, s, a1.data_ptr()))
+        _native.check(_native.lib().mrts_sample_actions_src(st, m.data_ptr(), g.source_unit_mask.data_ptr(), 256, 256, seed, s,
+                                                            a2.data_ptr()))
+        assert torch.equal(a1, a2), f"step {s}"
+        if s % 20 == 0:
+            np.testing.assert_array_equal(a2.cpu().numpy(), sample_actions(m.cpu().numpy(), 0x0123456789ABCDEF + s, s))
+        g.step(a2)
+
+
+@pytest.mark.parametrize("rows", [1, 37, 63, 64, 65, 255, 256, 257, 1000])
+def test_source_guided_sampler_ragged_rows(rows):
+    """Waves of 64 rows: partial last wave, odd int64 tails, many source rows
+    per wave (more than one round of four cooperative row loads)."""
+    import ctypes
+
+    from gym_microrts import _native
+    from oracle_py import sample_actions
+
+    torch = _torch()
+    rng = np.random.default_rng(rows)
+    m = (rng.random((1, rows, 78)) < 0.2).astype(np.int32)
+    m[0, ::3] = 0
+    src = (m.sum(-1) > 0).astype(np.int32)
+    m[0, :, 0] |= src[0]   # getMasks: a source cell always has its NOOP bit
+    md, sd = torch.from_numpy(m).cuda(), torch.from_numpy(src).cuda()
+    out = torch.full((1, rows, 7), -1, dtype=torch.int64, device="cuda")
+    _native.check(_native.lib().mrts_sample_actions_src(torch.cuda.current_stream().cuda_stream, md.data_ptr(), sd.data_ptr(), 1,
+                                                        rows, ctypes.c_uint64(42), 7, out.data_ptr()))
+    np.testing.assert_array_equal(out.cpu().numpy(), sample_actions(m, 42, 7))
 
 
 def test_float_obs_equals_int_obs():
