@@ -57,6 +57,19 @@ enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_U
        SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_WORDS = 32 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// 16-byte store of an output row segment (obs / masks: written once, read by
+// the consumer after the kernel).  MRTS_NT_STORES selects non-temporal stores.
+__device__ __forceinline__ void st16(void* dst, int a, int b, int c, int d) {
+    v4i v = {a, b, c, d};
+#ifdef MRTS_NT_STORES
+    __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(dst));
+#else
+    *reinterpret_cast<v4i*>(dst) = v;
+#endif
+}
+
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
@@ -236,20 +249,17 @@ __device__ __forceinline__ void write_obs(const EngineParams& p, const Lds& L, i
     OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)env * HW * P;
     const int total = HW * P;
     if ((total & 3) == 0) {
-        using V4 = typename std::conditional<std::is_same<OT, float>::value, float4, int4>::type;
-        V4* o4 = reinterpret_cast<V4*>(out);
+        constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
         for (int k = threadIdx.x; k < total / 4; k += NT) {
             int e = 4 * k;
             int c = e / P, pl = e - c * P;
-            OT v[4];
+            int v[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                v[j] = (OT)((L.aux[c] >> pl) & 1u);
+                v[j] = ((L.aux[c] >> pl) & 1u) ? ONE : 0;
                 if (++pl == P) { pl = 0; c++; }
             }
-            V4 w;
-            w.x = v[0]; w.y = v[1]; w.z = v[2]; w.w = v[3];
-            o4[k] = w;
+            st16(out + e, v[0], v[1], v[2], v[3]);
         }
     } else {
         for (int e = threadIdx.x; e < total; e += NT) out[e] = (OT)((L.aux[e / P] >> (e % P)) & 1u);
@@ -335,7 +345,6 @@ __device__ __forceinline__ void write_masks(const EngineParams& p, const Lds& L,
         int32_t* out = p.mask + (size_t)env * HW * MRTS_MASK_CH;
         const int total = HW * MRTS_MASK_CH;
         if ((total & 3) == 0) {
-            int4* o4 = reinterpret_cast<int4*>(out);
             for (int k = threadIdx.x; k < total / 4; k += NT) {
                 int e = 4 * k;
                 int c = e / MRTS_MASK_CH, ch = e - c * MRTS_MASK_CH;
@@ -346,7 +355,7 @@ __device__ __forceinline__ void write_masks(const EngineParams& p, const Lds& L,
                     v4[j] = (int)((L.mbits[3 * c + (b >> 5)] >> (b & 31)) & 1u);
                     if (++ch == MRTS_MASK_CH) { ch = 0; c++; }
                 }
-                o4[k] = make_int4(v4[0], v4[1], v4[2], v4[3]);
+                st16(out + e, v4[0], v4[1], v4[2], v4[3]);
             }
         } else {
             for (int e = threadIdx.x; e < total; e += NT) {
@@ -594,8 +603,11 @@ __device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s
     }
 }
 
+#ifndef MRTS_STEP_MIN_WAVES
+#define MRTS_STEP_MIN_WAVES 1
+#endif
 template <int NT, int P, typename OT>
-__global__ __launch_bounds__(NT) void k_step(EngineParams p) {
+__global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
@@ -864,7 +876,9 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
 #endif
     // (8) getMasks of the next tick (bound mask outputs): every read of this
     //     game's source rows (phase 1) is behind the barriers above
+#ifndef MRTS_EXP_NOMASKW
     if (p.mask) write_masks<NT>(p, L, G);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -929,7 +943,6 @@ constexpr int SW = MRTS_SAMPLE_ROWS;                     // rows per group (one 
 constexpr int SWAVES = 4;                                // waves per workgroup
 constexpr int SNV = (SW * MRTS_MASK_CH / 4 + 63) / 64;   // dwordx4 loads per lane per group (10)
 
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 struct SampleBuf {
     int4 v[SNV];

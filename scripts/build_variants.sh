@@ -8,11 +8,7 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude 
 S="$C/mrts_engine.hip $C/mrts_bots.hip $C/mrts_capi.cpp"
 build() { name=$1; shift; /opt/rocm/bin/hipcc $F "$@" -o scripts/_exp/lib_$name.so $S & }
 build base
-build noobs -DMRTS_EXP_NOOBS
-build s32_b8 -DMRTS_SAMPLE_BLOCKS_PER_CU=8
-build s32_b16 -DMRTS_SAMPLE_BLOCKS_PER_CU=16
-build s32_b32 -DMRTS_SAMPLE_BLOCKS_PER_CU=32
-build s32_b64 -DMRTS_SAMPLE_BLOCKS_PER_CU=64
-build s16_b16 -DMRTS_SAMPLE_ROWS=16 -DMRTS_SAMPLE_BLOCKS_PER_CU=16
+build w8 -DMRTS_STEP_MIN_WAVES=8
+build w8nt -DMRTS_STEP_MIN_WAVES=8 -DMRTS_NT_STORES
 wait
 ls -la scripts/_exp

@@ -32,7 +32,8 @@ def child(lib_path, workload):
     a = A()
     a.envs_per_gpu, a.max_steps, a.seed, a.warmup, a.steps, a.no_kernel_events = 8192, 2000, 1, 30, 100, False
     a.workload = workload
-    elapsed, kern, flags, hw, G, N, P = bench.run_gpu(a, 0, 1, 0)
+    a.no_eager_masks, a.sampler = False, "src"
+    elapsed, kern, flags, hw, G, N, P, _ = bench.run_gpu(a, 0, 1, 0)
     print(json.dumps({"lib": os.path.basename(lib_path), "workload": workload, "ms_per_step": 1e3 * elapsed / a.steps,
                       "kernels_ms": kern, "flags": flags}))
 

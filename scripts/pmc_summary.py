@@ -45,7 +45,7 @@ def main(src, dst):
             continue
         f = sum(fetch[k]) / len(fetch[k]) if fetch.get(k) else None
         w = sum(write[k]) / len(write[k]) if write.get(k) else None
-        wide = any(k.startswith(p) for p in WIDE_LOAD_KERNELS)
+        wide = k.split("<")[0] in WIDE_LOAD_KERNELS   # k_sample_src: 4-B loads, uncalibrated
         fc = None if f is None else (2.0 * f if wide else f)
         res[k] = {"fetch_bytes_raw": f, "fetch_bytes": fc, "write_bytes": w,
                   "hbm_bytes": None if fc is None or w is None else fc + w,
