@@ -148,6 +148,11 @@ int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int
 int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t num_envs, int32_t hw,
                             uint64_t seed, uint32_t step, int64_t *actions);
 
+/* render("rgb_array") (vec_env.py:1075-1084): the game of `env` drawn into a
+ * device frame rgb [size][size][3] uint8 (RGB; the reference returns 640 x 640).
+ * Drawing rules: DESIGN.md §4c (the Java panel is absent; parity unpinned). */
+int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t size);
+
 /* Engine invariant violations recorded on the device (OR over games). */
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out);
 

@@ -443,6 +443,15 @@ int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source) {
     return MRTS_OK;
 }
 
+int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t size) {
+    if (!bound(h) || !rgb) return fail(h, MRTS_ESTATE, "render: workspace not bound or rgb null");
+    if (env < 0 || env >= h->nenvs) return fail(h, MRTS_EINVAL, "render: env out of range");
+    if (size < h->W || size < h->H || size > 8192) return fail(h, MRTS_EINVAL, "render: size must be in [max(H, W), 8192]");
+    const int game = env < h->nsp ? env / 2 : h->nsp / 2 + (env - h->nsp);
+    hipError_t e = mrts_engine_render(&h->base, (hipStream_t)stream, game, h->game_map[game], size, rgb);
+    return e ? hip_fail(h, e, "render launch") : MRTS_OK;
+}
+
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {
     if (!bound(h) || !flags_out) return fail(h, MRTS_ESTATE, "error_flags: not bound");
     std::vector<int32_t> genv((size_t)h->ngames * MRTS_GENV_WORDS);

@@ -43,6 +43,7 @@ hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *ra
 hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
 hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n, int hw, uint64_t seed, uint32_t step, int64_t *act,
                                   hipStream_t s);
+hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, int map, int size, uint8_t *rgb);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);
 }

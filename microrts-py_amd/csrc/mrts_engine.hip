@@ -882,6 +882,65 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
 }
 
 // ---------------------------------------------------------------------------
+// render("rgb_array") (vec_env.py:1075-1084): a size x size RGB frame of one
+// game, one lane per pixel.  The Java PhysicalGameStatePanel is absent, so the
+// drawing rules are this engine's own (restated pixel for pixel
+// by oracle_py.render_frame): cells of cs = size / max(W, H) pixels centred in
+// the frame, grid lines, walls, buildings / resources as inset squares, mobile
+// units as discs, an owner-coloured rim (player 0 blue, player 1 red) and a
+// hit-point bar on damaged units.
+__device__ __forceinline__ uint32_t render_type_rgb(int t) {
+    switch (t) {
+    case RESOURCE: return 0x00A000u;
+    case BASE: return 0xFFFFFFu;
+    case BARRACKS: return 0xA0A0A0u;
+    case WORKER: return 0x808080u;
+    case LIGHT: return 0xFF8000u;
+    case HEAVY: return 0xFFFF00u;
+    default: return 0x00FFFFu;   // RANGED
+    }
+}
+
+__global__ __launch_bounds__(256) void k_render(const int4* __restrict__ cells, const uint8_t* __restrict__ wall, int W, int H,
+                                              int size, uint8_t* __restrict__ rgb) {
+    const int pix = blockIdx.x * 256 + threadIdx.x;
+    if (pix >= size * size) return;
+    const int px = pix % size, py = pix / size;
+    const int cs = size / max(W, H), ox = (size - cs * W) / 2, oy = (size - cs * H) / 2;
+    uint32_t col = 0;
+    const int gx = px - ox, gy = py - oy;
+    if (gx >= 0 && gy >= 0 && gx < cs * W && gy < cs * H) {
+        const int cx = gx / cs, cy = gy / cs, lx = gx - cx * cs, ly = gy - cy * cs, c = cy * W + cx;
+        col = wall[c] ? 0x205020u : 0u;
+        if (lx == 0 || ly == 0) col = 0x303030u;
+        const uint32_t u = (uint32_t)cells[c].x;
+        if (u != 0) {
+            const int t = u_type(u), ow = u_owner(u), m = cs / 8, b = max(1, cs / 16);
+            const bool building = t == RESOURCE || t == BASE || t == BARRACKS;
+            bool inside, rim;
+            if (building) {
+                inside = lx >= m && ly >= m && lx < cs - m && ly < cs - m;
+                rim = lx < m + b || ly < m + b || lx >= cs - m - b || ly >= cs - m - b;
+            } else {
+                const int r2 = cs * 3 / 4, dx = 2 * lx + 1 - cs, dy = 2 * ly + 1 - cs, d2 = dx * dx + dy * dy;
+                inside = d2 <= r2 * r2;
+                rim = d2 > (r2 - 2 * b) * (r2 - 2 * b);
+            }
+            if (inside) {
+                col = render_type_rgb(t);
+                if (rim && ow >= 0) col = ow == 0 ? 0x0000FFu : 0xFF0000u;
+            }
+            const int hp = u_hp(u), mhp = ut_hp(t);
+            if (t != RESOURCE && hp < mhp && ly >= cs - m - 2 * b && ly < cs - m && lx >= m && lx < m + (cs - 2 * m) * hp / mhp)
+                col = 0xFF0000u;
+        }
+    }
+    rgb[3 * (size_t)pix] = (uint8_t)(col >> 16);
+    rgb[3 * (size_t)pix + 1] = (uint8_t)(col >> 8);
+    rgb[3 * (size_t)pix + 2] = (uint8_t)col;
+}
+
+// ---------------------------------------------------------------------------
 // Counter-based masked sampler (hello_world.py:27-64 semantics), Philox4x32-10
 // keyed (seed) with counter (cell, env, step, half) -- identical stream to the
 // oracle's ovec_sample_actions.  One lane per (env, cell).
@@ -1165,6 +1224,12 @@ hipError_t mrts_engine_sample_src(const int32_t* mask, const int32_t* src, int n
     if (rows == 0) return hipSuccess;
     const long long blocks = (rows + 64 * mrts::SR_WAVES - 1) / (64 * mrts::SR_WAVES);
     hipLaunchKernelGGL(mrts::k_sample_src, dim3((unsigned)blocks), dim3(64 * mrts::SR_WAVES), 0, s, mask, src, n, hw, seed, step, act);
+    return hipGetLastError();
+}
+hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, int map, int size, uint8_t* rgb) {
+    const int nblk = (size * size + 255) / 256;
+    hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->HW, p->map_wall + (size_t)map * p->HW,
+                       p->W, p->H, size, rgb);
     return hipGetLastError();
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {

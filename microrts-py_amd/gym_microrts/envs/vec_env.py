@@ -19,6 +19,7 @@ Return types
 """
 import json
 import os
+import warnings
 import xml.etree.ElementTree as ET
 from enum import Enum
 from itertools import cycle
@@ -30,6 +31,8 @@ import gym_microrts
 from gym_microrts import _native
 from gym_microrts._native import MicroRTSError, MicroRTSNotImplemented
 from gym_microrts._spaces import Box, Discrete, MultiDiscrete
+
+RENDER_SIZE = 640   # vec_env.py:1083: Image.frombytes("RGB", (640, 640), ...)
 
 RF_NAMES = [
     "WinLossRewardFunction",
@@ -374,7 +377,21 @@ class MicroRTSGridModeVecEnv:
         return None
 
     def render(self, mode="human"):
-        raise MicroRTSNotImplemented("render() (Java Swing / 640x640 RGB frames) is out of scope (DESIGN.md §8)")
+        """vec_env.py:1075-1084 on render_client = game 0 (selfPlayClients[0], else
+        clients[0]: env 0 either way).  "rgb_array": a 640x640x3 uint8 RGB frame drawn
+        on the device (k_render).  "human": the Java Swing window has no
+        counterpart on a headless GPU host; warns once and draws nothing."""
+        if mode == "human":
+            if not getattr(self, "_human_warned", False):
+                warnings.warn("render(mode='human') has no display on the GPU engine; use render('rgb_array') frames")
+                self._human_warned = True
+            return None
+        if mode != "rgb_array":
+            raise ValueError(f"unsupported render mode {mode!r}")
+        if getattr(self, "_frame", None) is None:
+            self._frame = torch.empty((RENDER_SIZE, RENDER_SIZE, 3), dtype=torch.uint8, device=self.device)
+        _native.check(_native.lib().mrts_render(self._h, self._stream(), 0, self._frame.data_ptr(), RENDER_SIZE), self._h, "render")
+        return self._frame.cpu().numpy()
 
     def error_flags(self):
         import ctypes

@@ -187,3 +187,45 @@ def sample_actions(masks78, seed, step):
     out = np.zeros((n, hw, 7), np.int64)
     lib().ovec_sample_actions(ptr(m), n, hw, ctypes.c_uint64(seed), ctypes.c_uint32(step), ptr(out))
     return out
+
+
+# render("rgb_array") drawing rules, restated in numpy from the
+# rule list -- the device k_render must match it pixel for pixel.
+_RENDER_RGB = {0: 0x00A000, 1: 0xFFFFFF, 2: 0xA0A0A0, 3: 0x808080, 4: 0xFF8000, 5: 0xFFFF00, 6: 0x00FFFF}
+_MAX_HP = {0: 1, 1: 10, 2: 4, 3: 1, 4: 4, 5: 4, 6: 1}
+
+
+def render_frame(cells, wall, W, H, size=640):
+    """cells: OracleVecEnv.dump_cells(g) (type, player, hp, ...) per cell; wall: u8 [H*W]."""
+    col = np.zeros((size, size), np.int64)
+    cs = size // max(W, H)
+    ox, oy = (size - cs * W) // 2, (size - cs * H) // 2
+    py, px = np.mgrid[0:size, 0:size]
+    gx, gy = px - ox, py - oy
+    ing = (gx >= 0) & (gy >= 0) & (gx < cs * W) & (gy < cs * H)
+    cx, cy = np.where(ing, gx // cs, 0), np.where(ing, gy // cs, 0)
+    lx, ly = gx - cx * cs, gy - cy * cs
+    c = cy * W + cx
+    wall = np.asarray(wall).reshape(-1)
+    col = np.where(ing, np.where(wall[c] != 0, 0x205020, 0), 0)
+    col = np.where(ing & ((lx == 0) | (ly == 0)), 0x303030, col)
+    t, owner, hp = cells[c, 0], cells[c, 1], cells[c, 2]
+    m, b = cs // 8, max(1, cs // 16)
+    building = (t == 0) | (t == 1) | (t == 2)
+    sq_in = (lx >= m) & (ly >= m) & (lx < cs - m) & (ly < cs - m)
+    sq_rim = (lx < m + b) | (ly < m + b) | (lx >= cs - m - b) | (ly >= cs - m - b)
+    r2 = cs * 3 // 4
+    d2 = (2 * lx + 1 - cs) ** 2 + (2 * ly + 1 - cs) ** 2
+    ci_in, ci_rim = d2 <= r2 * r2, d2 > (r2 - 2 * b) ** 2
+    inside = np.where(building, sq_in, ci_in)
+    rim = np.where(building, sq_rim, ci_rim)
+    unit = ing & (t >= 0)
+    fill = np.vectorize(lambda k: _RENDER_RGB.get(int(k), 0))(np.clip(t, 0, 6))
+    rimc = np.where(owner == 0, 0x0000FF, 0xFF0000)
+    ucol = np.where(rim & (owner >= 0), rimc, fill)
+    col = np.where(unit & inside, ucol, col)
+    mhp = np.vectorize(lambda k: _MAX_HP.get(int(k), 1))(np.clip(t, 0, 6))
+    bar = unit & (t != 0) & (hp < mhp) & (ly >= cs - m - 2 * b) & (ly < cs - m) & (lx >= m) & (lx < m + (cs - 2 * m) * hp // mhp)
+    col = np.where(bar, 0xFF0000, col)
+    rgb = np.stack([(col >> 16) & 255, (col >> 8) & 255, col & 255], -1).astype(np.uint8)
+    return rgb
