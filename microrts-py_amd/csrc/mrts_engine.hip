@@ -21,6 +21,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "mrts_engine.h"
 #include "mrts_layout.h"
@@ -43,7 +45,7 @@ struct Lds {
     int32_t* blist;  // the bot's PlayerAction order (bot games)
     int32_t* blist0; // player 0's bot PlayerAction (bot-vs-bot games)
     int4* snap;      // ready-action snapshots
-    uint32_t* mbits; // mask bits, 3 words per cell (mask kernel)
+    uint32_t* outw;  // emit_outputs words: aliases resv .. snap (32 B per cell)
     uint8_t* wall;
     unsigned long long* ballot;
     uint32_t* posbits;
@@ -76,7 +78,6 @@ __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     size_t b = 0;
     b += a16(4 * (size_t)HW) * 10; // unit uid act seq aux resv list prod blist blist0
     b += a16(16 * (size_t)HW);     // snap
-    b += a16(12 * (size_t)HW);     // mbits
     b += a16((size_t)HW);          // wall
     b += a16(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     b += a16(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
@@ -101,7 +102,7 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     L.blist = (int32_t*)take(4 * (size_t)HW);
     L.blist0 = (int32_t*)take(4 * (size_t)HW);
     L.snap = (int4*)take(16 * (size_t)HW);
-    L.mbits = (uint32_t*)take(12 * (size_t)HW);
+    L.outw = (uint32_t*)L.resv;   // resv, list, prod, blist, blist0, snap: >= 36 B per cell, contiguous
     L.wall = (uint8_t*)take((size_t)HW);
     L.ballot = (unsigned long long*)take(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     L.posbits = (uint32_t*)take(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
@@ -229,46 +230,89 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
     __syncthreads();
 }
 
+// All outputs of one game once its state is final.  Phase A (lane per cell):
+// every view's one-hot word and, with `masks`, its getMasks(0) 79-bit word
+// (+ the source channel, written straight out) into LDS; one barrier; phase B:
+// the views' obs rows, then their mask rows, streamed with 16-byte stores and no
+// further barrier (the envs of a game are adjacent: a selfplay pair 2k, 2k+1
+// writes one contiguous run).  The words live in the region of the step's
+// scratch lists (resv .. snap), dead by now.
 template <int NT, int P, typename OT>
-__device__ __forceinline__ void write_obs(const EngineParams& p, const Lds& L, int env, int player) {
-    const int HW = p.HW;
-    if (P == 31) {
-        const int nw = HW / 32 + 1;
-        const uint32_t* vme = L.vis + player * nw;
-        const uint32_t* vop = L.vis + (1 - player) * nw;
-        for (int c = threadIdx.x; c < HW; c += NT) {
-            uint32_t u = L.unit[c];
-            bool shown = u == 0 || u_owner(u) == player || ((vme[c >> 5] >> (c & 31)) & 1u);
-            bool opp = (vop[c >> 5] >> (c & 31)) & 1u;
-            L.aux[c] = cell_onehot(u, L.act[c], L.wall[c], player, P, shown, opp);
-        }
-    } else {
-        for (int c = threadIdx.x; c < HW; c += NT) L.aux[c] = cell_onehot(L.unit[c], L.act[c], L.wall[c], player);
-    }
-    __syncthreads();
-    OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)env * HW * P;
-    const int total = HW * P;
-    if ((total & 3) == 0) {
-        constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
-        for (int k = threadIdx.x; k < total / 4; k += NT) {
-            int e = 4 * k;
-            int c = e / P, pl = e - c * P;
-            int v[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                v[j] = ((L.aux[c] >> pl) & 1u) ? ONE : 0;
-                if (++pl == P) { pl = 0; c++; }
+__device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks) {
+    const int HW = p.HW, NV = G.nviews;
+    uint32_t* ow = L.outw;            // [NV][HW]    one-hot bits
+    uint32_t* mw = L.outw + 2 * HW;   // [NV][HW][3] mask bits (bit 0 = source)
+    const Grid gd{p.W, p.H, HW};
+    if (obs && P == 31) compute_vis<NT>(p, L);
+    const int nw = HW / 32 + 1;
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        const uint32_t u = L.unit[c], a = L.act[c];
+        const uint8_t wl = L.wall[c];
+        for (int v = 0; v < NV; v++) {
+            if (obs) {
+                if (P == 31) {
+                    const bool shown = u == 0 || u_owner(u) == v || ((L.vis[v * nw + (c >> 5)] >> (c & 31)) & 1u);
+                    const bool opp = (L.vis[(1 - v) * nw + (c >> 5)] >> (c & 31)) & 1u;
+                    ow[v * HW + c] = cell_onehot(u, a, wl, v, P, shown, opp);
+                } else {
+                    ow[v * HW + c] = cell_onehot(u, a, wl, v);
+                }
             }
-            st16(out + e, v[0], v[1], v[2], v[3]);
+            if (masks) {
+                uint32_t m[3];
+                cell_mask(gd, c, v, L.unit, L.act, L.wall, v == 0 ? L.sc[SC_RES0] : L.sc[SC_RES1], m);
+                mw[3 * (v * HW + c)] = m[0];
+                mw[3 * (v * HW + c) + 1] = m[1];
+                mw[3 * (v * HW + c) + 2] = m[2];
+                p.src_out[(size_t)(G.env0 + v) * HW + c] = (int32_t)(m[0] & 1u);
+            }
         }
-    } else {
-        for (int e = threadIdx.x; e < total; e += NT) out[e] = (OT)((L.aux[e / P] >> (e % P)) & 1u);
     }
     __syncthreads();
+    if (obs) {
+        OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P;
+        const int total = NV * HW * P;
+        if (((HW * P) & 3) == 0) {   // every env's rows start 16-B aligned
+            constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
+            for (int k = threadIdx.x; k < total / 4; k += NT) {
+                const int e = 4 * k;
+                int c = e / P, pl = e - c * P;
+                int v[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    v[j] = ((ow[c] >> pl) & 1u) ? ONE : 0;
+                    if (++pl == P) { pl = 0; c++; }
+                }
+                st16(out + e, v[0], v[1], v[2], v[3]);
+            }
+        } else {
+            for (int e = threadIdx.x; e < total; e += NT) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
+        }
+    }
+    if (masks) {
+        int32_t* out = p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH;
+        const int total = NV * HW * MRTS_MASK_CH;
+        if ((HW & 1) == 0) {   // HW * 78 % 4 == 0: every env's rows start 16-B aligned
+            for (int k = threadIdx.x; k < total / 4; k += NT) {
+                const int e = 4 * k;
+                int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
+                int v4[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int b = ch + 1;
+                    v4[j] = (int)((mw[3 * r + (b >> 5)] >> (b & 31)) & 1u);
+                    if (++ch == MRTS_MASK_CH) { ch = 0; r++; }
+                }
+                st16(out + e, v4[0], v4[1], v4[2], v4[3]);
+            }
+        } else {
+            for (int e = threadIdx.x; e < total; e += NT) {
+                const int r = e / MRTS_MASK_CH, b = e % MRTS_MASK_CH + 1;
+                out[e] = (int)((mw[3 * r + (b >> 5)] >> (b & 31)) & 1u);
+            }
+        }
+    }
 }
-
-template <int NT>
-__device__ __forceinline__ void write_masks(const EngineParams& p, const Lds& L, const Game& G);
 
 // ---------------------------------------------------------------------------
 // Reset kernel: every game (or the listed ones) back to its map; obs out.
@@ -284,9 +328,7 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
     __syncthreads();
     store_game<NT>(p, L, g);
     Game G = game_of(p, g);
-    if (P == 31) compute_vis<NT>(p, L);
-    for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
-    if (p.mask) write_masks<NT>(p, L, G);
+    emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -321,52 +363,6 @@ __global__ __launch_bounds__(NT) void k_raw(EngineParams p, int32_t* raw) {
 }
 
 // ---------------------------------------------------------------------------
-// JNIGridnetVecClient.getMasks(0) of the game in LDS -> [N][HW][78] + source
-// [N][HW] of every view: per-cell 79-bit words in LDS, then 16-byte stores.
-// Shared by k_masks (a standalone getMasks) and by k_step / k_reset, which
-// write the masks of the state they leave behind when mask outputs are bound
-// (mrts_bind_mask_outputs): the same bytes a following getMasks would write.
-template <int NT>
-__device__ __forceinline__ void write_masks(const EngineParams& p, const Lds& L, const Game& G) {
-    const int HW = p.HW;
-    Grid gd{p.W, p.H, HW};
-    for (int v = 0; v < G.nviews; v++) {
-        const int env = G.env0 + v, player = v;
-        const int res = player == 0 ? L.sc[SC_RES0] : L.sc[SC_RES1];
-        for (int c = threadIdx.x; c < HW; c += NT) {
-            uint32_t m[3];
-            cell_mask(gd, c, player, L.unit, L.act, L.wall, res, m);
-            L.mbits[3 * c] = m[0];
-            L.mbits[3 * c + 1] = m[1];
-            L.mbits[3 * c + 2] = m[2];
-            p.src_out[(size_t)env * HW + c] = (int32_t)(m[0] & 1u);
-        }
-        __syncthreads();
-        int32_t* out = p.mask + (size_t)env * HW * MRTS_MASK_CH;
-        const int total = HW * MRTS_MASK_CH;
-        if ((total & 3) == 0) {
-            for (int k = threadIdx.x; k < total / 4; k += NT) {
-                int e = 4 * k;
-                int c = e / MRTS_MASK_CH, ch = e - c * MRTS_MASK_CH;
-                int v4[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    int b = ch + 1;
-                    v4[j] = (int)((L.mbits[3 * c + (b >> 5)] >> (b & 31)) & 1u);
-                    if (++ch == MRTS_MASK_CH) { ch = 0; c++; }
-                }
-                st16(out + e, v4[0], v4[1], v4[2], v4[3]);
-            }
-        } else {
-            for (int e = threadIdx.x; e < total; e += NT) {
-                int c = e / MRTS_MASK_CH, b = e % MRTS_MASK_CH + 1;
-                out[e] = (int)((L.mbits[3 * c + (b >> 5)] >> (b & 31)) & 1u);
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // Mask kernel: JNIGridnetVecClient.getMasks(0) -> [N][HW][78] + source [N][HW]
 template <int NT>
 __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
@@ -374,7 +370,7 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
     Lds L = carve(smem, p.HW, p.W, NT);
     const int g = blockIdx.x;
     load_game<NT>(p, L, g);
-    write_masks<NT>(p, L, game_of(p, g));
+    emit_outputs<NT, 29, int32_t>(p, L, game_of(p, g), false, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -603,25 +599,104 @@ __device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s
     }
 }
 
+// Register prefetch of a game's state (maps with HW <= NT: one cell per lane):
+// issued before the current game's output stream, so the next game's state
+// round trip overlaps those stores instead of stalling the block.
+struct StatePf {
+    int4 cell;
+    int genv, src0, src1;
+};
+template <int NT>
+__device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, StatePf& pf) {
+    const Game G = game_of(p, g);
+    const int HW = p.HW, c = min((int)threadIdx.x, HW - 1);   // unconditional: counted waits
+    pf.cell = p.cells[(size_t)g * HW + c];
+    pf.src0 = p.src[(size_t)G.env0 * HW + c];
+    pf.src1 = p.src[(size_t)(G.env0 + G.nviews - 1) * HW + c];
+    pf.genv = p.genv[(size_t)g * MRTS_GENV_WORDS + min((int)threadIdx.x, MRTS_GENV_WORDS - 1)];
+}
+template <int NT>
+__device__ __forceinline__ void commit_game(const EngineParams& p, const Lds& L, const StatePf& pf) {
+    if (threadIdx.x < MRTS_GENV_WORDS) L.sc[threadIdx.x] = pf.genv;
+    __syncthreads();
+    const int HW = p.HW, map = L.sc[SC_MAP];
+    if ((int)threadIdx.x < HW) {
+        const int c = threadIdx.x;
+        L.unit[c] = (uint32_t)pf.cell.x;
+        L.uid[c] = pf.cell.y;
+        L.act[c] = (uint32_t)pf.cell.z;
+        L.seq[c] = (uint32_t)pf.cell.w;
+        L.wall[c] = p.map_wall[(size_t)map * HW + c];
+    }
+    __syncthreads();
+}
+
 #ifndef MRTS_STEP_MIN_WAVES
 #define MRTS_STEP_MIN_WAVES 1
 #endif
+// blockIdx -> game.  MRTS_EXP_XCD (experiment): consecutive workgroups go to
+// the 8 XCDs round-robin; remap so each XCD steps a contiguous range of games.
+__device__ __forceinline__ int step_game_index(int G) {
+#ifdef MRTS_EXP_XCD
+    if ((G & 7) == 0 && (int)gridDim.x == G) return (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+#endif
+    return blockIdx.x;
+}
+// One game per workgroup.  MRTS_STEP_PERSISTENT (experiment): the grid is
+// sized to the resident capacity (launch_step) and block b steps games b,
+// b + gridDim.x, ..., prefetching the next game's state during the current
+// game's output stream (measured: hipcc's allocation of the looped body takes
+// 164 VGPRs, occupancy 3 -- DESIGN.md §5).
 template <int NT, int P, typename OT>
 __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
-    const int g = blockIdx.x;
     const Grid gd{p.W, p.H, HW};
+#ifdef MRTS_EXP_FILL   // kernel-variant experiments only: zeros over one launch's output bytes, no loads
+    {
+        const v4i z = {0, 0, 0, 0};
+        if (MRTS_EXP_FILL == 1) {   // per game: its envs' obs + mask rows (k_step's pattern)
+            const Game G = game_of(p, step_game_index(p.G));
+            v4i* o = reinterpret_cast<v4i*>(reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P);
+            for (int k = threadIdx.x; k < G.nviews * HW * P / 4; k += NT) o[k] = z;
+            v4i* m = reinterpret_cast<v4i*>(p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH);
+            for (int k = threadIdx.x; k < G.nviews * HW * MRTS_MASK_CH / 4; k += NT) m[k] = z;
+        } else {                    // grid-stride over both arrays (a fill kernel's pattern)
+            const long long N = p.nsp + (p.G - p.nsp_games), st = (long long)gridDim.x * NT;
+            v4i* o = reinterpret_cast<v4i*>(p.obs);
+            for (long long k = (long long)blockIdx.x * NT + threadIdx.x; k < N * HW * P / 4; k += st) o[k] = z;
+            v4i* m = reinterpret_cast<v4i*>(p.mask);
+            for (long long k = (long long)blockIdx.x * NT + threadIdx.x; k < N * HW * MRTS_MASK_CH / 4; k += st) m[k] = z;
+        }
+        return;
+    }
+#endif
+    const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
+    StatePf pf;
+#ifdef MRTS_STEP_PERSISTENT
+    if (pf_ok && (int)blockIdx.x < p.G) prefetch_game<NT>(p, blockIdx.x, pf);
+    for (int g = blockIdx.x; g < p.G; g += gridDim.x) {
+#else
+    const int g = step_game_index(p.G);
+    if (pf_ok) prefetch_game<NT>(p, g, pf);
+    {
+#endif
     const Game G = game_of(p, g);
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
     // the source-unit rows of this lane's first cell, fetched in the same round
     // trip as the game state (the decode below needs both)
     int src_pre[2] = {0, 0};
-    if ((int)threadIdx.x < HW)
+    if (pf_ok) {
+        src_pre[0] = pf.src0;
+        src_pre[1] = pf.src1;
+    } else if ((int)threadIdx.x < HW) {
         for (int v = 0; v < G.nviews; v++) src_pre[v] = p.src[(size_t)(G.env0 + v) * HW + threadIdx.x];
+    }
     __syncthreads();
-    load_game<NT>(p, L, g);
+    if (pf_ok) commit_game<NT>(p, L, pf);
+    else load_game<NT>(p, L, g);
+#ifndef MRTS_EXP_NOLOGIC   // kernel-variant experiments only: state in, outputs out, no game logic
     const int time = L.sc[SC_TIME];
     // bot-vs-bot game (MicroRTSBotVecEnv): player 0's PlayerAction comes from k_bot too
     const bool bot0 = !G.selfplay && p.bot_ai0 && p.bot_ai0[g - p.nsp_games] >= 0;
@@ -868,17 +943,28 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
         L.sc[SC_STEPS] = steps;
     }
     __syncthreads();
+#endif
+#ifdef MRTS_STEP_PERSISTENT
+    // the next game's state: in flight while this game's outputs stream out
+    if (pf_ok && g + (int)gridDim.x < p.G) prefetch_game<NT>(p, g + gridDim.x, pf);
+#endif
     // (7) write back + one-hot observation of every view
     store_game<NT>(p, L, g);
-#ifndef MRTS_EXP_NOOBS   // kernel-variant experiments only (scripts/kernel_variants.py)
-    if (P == 31) compute_vis<NT>(p, L);
-    for (int v = 0; v < G.nviews; v++) write_obs<NT, P, OT>(p, L, G.env0 + v, v);
+    // + getMasks of the next tick (bound mask outputs): every read of this
+    //   game's source rows (phase 1) is behind the barriers above
+#ifdef MRTS_EXP_NOOBS   // kernel-variant experiments only (scripts/kernel_variants.py)
+    constexpr bool kObs = false;
+#else
+    constexpr bool kObs = true;
 #endif
-    // (8) getMasks of the next tick (bound mask outputs): every read of this
-    //     game's source rows (phase 1) is behind the barriers above
-#ifndef MRTS_EXP_NOMASKW
-    if (p.mask) write_masks<NT>(p, L, G);
+#ifdef MRTS_EXP_NOMASKW
+    constexpr bool kMasks = false;
+#else
+    constexpr bool kMasks = true;
 #endif
+    emit_outputs<NT, P, OT>(p, L, G, kObs, kMasks && p.mask != nullptr);
+    __syncthreads();   // LDS is reused by the next game
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1159,6 +1245,38 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
 
 // ---------------------------------------------------------------------------
 // launchers
+
+#ifdef MRTS_STEP_PERSISTENT
+// Resident capacity of a kernel on the current device (blocks per CU x CUs),
+// cached per (kernel, LDS bytes, device).
+static int resident_blocks(const void* kernel, int NT, size_t sh) {
+    struct Entry { const void* k; size_t sh; int dev, blocks; };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lock(mu);
+    for (const Entry& e : cache)
+        if (e.k == kernel && e.sh == sh && e.dev == dev) return e.blocks;
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, NT, sh) != hipSuccess)
+        return 0;
+    cache.push_back({kernel, sh, dev, cus * per});
+    return cus * per;
+}
+#endif
+
+template <typename K>
+static void launch_step(K kernel, int NT, size_t sh, hipStream_t s, const EngineParams& p) {
+    int grid = p.G;
+#ifdef MRTS_STEP_PERSISTENT
+    const int cap = resident_blocks(reinterpret_cast<const void*>(kernel), NT, sh);
+    if (cap > 0) grid = std::min(grid, cap);
+#endif
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(NT), sh, s, p);
+}
+
 template <int NT>
 static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
     size_t sh = lds_bytes(p.HW, p.W, NT);
@@ -1177,17 +1295,20 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
     } else {
         if (p.partial_obs) {
-            if (p.obs_float) hipLaunchKernelGGL((k_step<NT, 31, float>), dim3(grid), dim3(NT), sh, s, p);
-            else hipLaunchKernelGGL((k_step<NT, 31, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+            if (p.obs_float) launch_step(k_step<NT, 31, float>, NT, sh, s, p);
+            else launch_step(k_step<NT, 31, int32_t>, NT, sh, s, p);
         } else {
-            if (p.obs_float) hipLaunchKernelGGL((k_step<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p);
-            else hipLaunchKernelGGL((k_step<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+            if (p.obs_float) launch_step(k_step<NT, 29, float>, NT, sh, s, p);
+            else launch_step(k_step<NT, 29, int32_t>, NT, sh, s, p);
         }
     }
     return hipGetLastError();
 }
 
 static hipError_t dispatch(const EngineParams& p, int kind, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
+#ifdef MRTS_FORCE_NT   // kernel-variant experiments only: workgroup size independent of the map
+    return launch_all<MRTS_FORCE_NT>(p, kind, s, games, maps, count);
+#endif
     if (p.HW <= 64) return launch_all<64>(p, kind, s, games, maps, count);
     if (p.HW <= 128) return launch_all<128>(p, kind, s, games, maps, count);
     return launch_all<256>(p, kind, s, games, maps, count);

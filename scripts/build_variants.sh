@@ -8,7 +8,8 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude 
 S="$C/mrts_engine.hip $C/mrts_bots.hip $C/mrts_capi.cpp"
 build() { name=$1; shift; /opt/rocm/bin/hipcc $F "$@" -o scripts/_exp/lib_$name.so $S & }
 build base
-build w8 -DMRTS_STEP_MIN_WAVES=8
-build w8nt -DMRTS_STEP_MIN_WAVES=8 -DMRTS_NT_STORES
+build xcd -DMRTS_EXP_XCD
+build fill1 -DMRTS_EXP_FILL=1
+build fill1xcd -DMRTS_EXP_FILL=1 -DMRTS_EXP_XCD
 wait
 ls -la scripts/_exp

@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXP = os.path.join(REPO, "scripts", "_exp")
 
 
-def child(lib_path, workload):
+def child(lib_path, workload, envs=8192):
     sys.path.insert(0, os.path.join(REPO, "microrts-py_amd"))
     sys.path.insert(0, REPO)
     import numpy as np
@@ -30,24 +30,43 @@ def child(lib_path, workload):
         pass
 
     a = A()
-    a.envs_per_gpu, a.max_steps, a.seed, a.warmup, a.steps, a.no_kernel_events = 8192, 2000, 1, 30, 100, False
+    a.envs_per_gpu, a.max_steps, a.seed, a.warmup, a.steps, a.no_kernel_events = int(envs), 2000, 1, 30, 100, False
     a.workload = workload
-    a.no_eager_masks, a.sampler = False, "src"
+    a.no_eager_masks, a.sampler, a.event_every = False, "src", 1
     elapsed, kern, flags, hw, G, N, P, _ = bench.run_gpu(a, 0, 1, 0)
-    print(json.dumps({"lib": os.path.basename(lib_path), "workload": workload, "ms_per_step": 1e3 * elapsed / a.steps,
+    print(json.dumps({"lib": os.path.basename(lib_path), "workload": workload, "envs": int(envs), "ms_per_step": 1e3 * elapsed / a.steps,
                       "kernels_ms": kern, "flags": flags}))
 
 
+def fill_rate(nbytes=948428800, reps=30):
+    """Write ceiling of this box: torch's fill kernel over the bytes one k_step launch writes."""
+    import torch
+
+    buf = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        buf.fill_(0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        buf.fill_(1)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    print(json.dumps({"fill_bytes": nbytes, "fill_ms": ms, "fill_TBps": nbytes / ms / 1e9}))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--fill":
+        fill_rate()
+        return
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
-        child(sys.argv[2], sys.argv[3])
+        child(*sys.argv[2:])
         return
     names = sys.argv[1:] or sorted(f[4:-3] for f in os.listdir(EXP) if f.startswith("lib_"))
     for n in names:
-        wl = "selfplay"
-        if ":" in n:
-            n, wl = n.split(":")
-        out = subprocess.run([sys.executable, __file__, "--child", os.path.join(EXP, f"lib_{n}.so"), wl],
+        parts = n.split(":")   # name[:workload[:envs]]
+        n, wl, envs = parts[0], (parts[1] if len(parts) > 1 else "") or "selfplay", parts[2] if len(parts) > 2 else "8192"
+        out = subprocess.run([sys.executable, __file__, "--child", os.path.join(EXP, f"lib_{n}.so"), wl, envs],
                              capture_output=True, text=True, timeout=300)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         print(line[-1] if line else f"{n}: FAILED {out.stderr[-800:]}", flush=True)
