@@ -7,9 +7,8 @@ C=microrts-py_amd/csrc
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$C -shared"
 S="$C/mrts_engine.hip $C/mrts_bots.hip $C/mrts_capi.cpp"
 build() { name=$1; shift; /opt/rocm/bin/hipcc $F "$@" -o scripts/_exp/lib_$name.so $S & }
-build base
-build xcd -DMRTS_EXP_XCD
-build fill1 -DMRTS_EXP_FILL=1
-build fill1xcd -DMRTS_EXP_FILL=1 -DMRTS_EXP_XCD
+build simple -DMRTS_SAMPLE_SRC_SIMPLE
+build s2flat -DMRTS_SAMPLE_SRC_BLOCKS_PER_CU=1000000
+build s2b32 -DMRTS_SAMPLE_SRC_BLOCKS_PER_CU=32
 wait
 ls -la scripts/_exp
