@@ -1,0 +1,191 @@
+"""A GridNet PPO driver over the MI355X engine (BASELINE.json configs[3]).
+
+The reference trains with experiments/ppo_gridnet.py, whose third-party imports
+(gym, stable_baselines3, tensorboard) and whose file itself are absent from the
+GPU host.  This driver exercises the engine through exactly the calls that
+script makes on the env (SURVEY.md §8b callers; ppo_gridnet.py:364-383 the
+constructor, :421 reset, :460-466 get_action_mask, :475-476 step with host int64
+actions, numpy rewards / dones, infos[i]["raw_rewards"]) and runs the same
+algorithm family -- a GridNet encoder / deconvolution actor / critic, a masked
+categorical per action component, GAE and the clipped PPO objective -- so the
+rollout + update loop of configs[3] (16x16, partial_obs=True, 31 planes, 4096
+envs) runs end to end on the GPU.
+
+  --api numpy  : the reference's return contract (numpy obs / masks / rewards),
+                 i.e. the host round trips ppo_gridnet.py performs every step
+  --api tensor : return_tensors=True, every buffer stays in HBM
+
+  python examples/ppo_gridnet_driver.py --num-selfplay-envs 4096 --partial-obs --num-steps 8 --updates 2 --api tensor
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "microrts-py_amd"))
+
+from gym_microrts import microrts_ai  # noqa: E402
+from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv  # noqa: E402
+
+NVEC = [6, 4, 4, 4, 4, 7, 49]   # action_plane_space.nvec (vec_env.py:234)
+
+
+def orthogonal(m, gain=np.sqrt(2)):
+    nn.init.orthogonal_(m.weight, gain)
+    nn.init.zeros_(m.bias)
+    return m
+
+
+class GridNet(nn.Module):
+    """Encoder (two conv + max-pool stages, H x W -> H/4 x W/4), a transposed-conv
+    actor back to one 78-logit vector per cell, and a value head on the code."""
+
+    def __init__(self, planes, h, w):
+        super().__init__()
+        self.hw = h * w
+        self.enc = nn.Sequential(orthogonal(nn.Conv2d(planes, 32, 3, padding=1)), nn.MaxPool2d(3, 2, 1), nn.ReLU(),
+                                 orthogonal(nn.Conv2d(32, 64, 3, padding=1)), nn.MaxPool2d(3, 2, 1), nn.ReLU())
+        self.pi = nn.Sequential(orthogonal(nn.ConvTranspose2d(64, 32, 3, 2, 1, 1)), nn.ReLU(),
+                                orthogonal(nn.ConvTranspose2d(32, sum(NVEC), 3, 2, 1, 1)))
+        self.v = nn.Sequential(nn.Flatten(), orthogonal(nn.Linear(64 * (h // 4) * (w // 4), 128)), nn.ReLU(),
+                               orthogonal(nn.Linear(128, 1), 1.0))
+
+    def forward(self, obs):
+        z = self.enc(obs.permute(0, 3, 1, 2))
+        logits = self.pi(z).permute(0, 2, 3, 1).reshape(obs.shape[0] * self.hw, sum(NVEC))
+        return logits, self.v(z).squeeze(-1)
+
+
+def masked_log_softmax(logits, mask):
+    """Per action component: the logit where the mask allows it, -1e8 elsewhere
+    (ppo_gridnet's CategoricalMasked rule), as log-probabilities."""
+    out = []
+    for lg, mk in zip(torch.split(logits, NVEC, 1), torch.split(mask, NVEC, 1)):
+        out.append(torch.log_softmax(torch.where(mk.bool(), lg, torch.full_like(lg, -1e8)), -1))
+    return out
+
+
+def policy(net, obs, mask, hw, action=None):
+    logits, value = net(obs)
+    heads = masked_log_softmax(logits, mask.reshape(-1, sum(NVEC)))
+    if action is None:
+        action = torch.stack([torch.multinomial(h.exp(), 1).squeeze(-1) for h in heads], -1)
+    a = action.reshape(-1, len(NVEC))
+    logp = sum(h.gather(1, a[:, k:k + 1]).squeeze(-1) for k, h in enumerate(heads))
+    ent = sum(-(h.exp() * h).sum(-1) for h in heads)
+    return a.reshape(-1, hw, len(NVEC)), logp.reshape(-1, hw).sum(1), ent.reshape(-1, hw).sum(1), value
+
+
+def bot_list(n):
+    """ppo_gridnet.py:370-373's opponents (n >= 6 bot envs)."""
+    return ([microrts_ai.coacAI] * (n - 6) + [microrts_ai.randomBiasedAI] * min(n, 2) + [microrts_ai.lightRushAI] * min(n, 2)
+            + [microrts_ai.workerRushAI] * min(n, 2))
+
+
+def run(num_selfplay_envs=2, num_bot_envs=0, partial_obs=False, num_steps=16, updates=2, api="numpy", minibatches=4,
+        epochs=2, seed=1, device="cuda", log=print):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    dev = torch.device(device)
+    envs = MicroRTSGridModeVecEnv(num_selfplay_envs=num_selfplay_envs, num_bot_envs=num_bot_envs, partial_obs=partial_obs,
+                                  max_steps=2000, render_theme=2, ai2s=bot_list(num_bot_envs) if num_bot_envs else [],
+                                  map_paths=["maps/16x16/basesWorkers16x16A.xml"],
+                                  reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]),
+                                  cycle_maps=["maps/16x16/basesWorkers16x16A.xml"], device=dev, return_tensors=api == "tensor")
+    n, hw = envs.num_envs, envs.height * envs.width
+    h, w, planes = envs.observation_space.shape
+    net = GridNet(planes, h, w).to(dev)
+    opt = torch.optim.Adam(net.parameters(), lr=2.5e-4, eps=1e-5)
+    buf_obs = torch.zeros((num_steps, n, h, w, planes), device=dev)
+    buf_mask = torch.zeros((num_steps, n, hw, sum(NVEC)), device=dev)
+    buf_act = torch.zeros((num_steps, n, hw, len(NVEC)), dtype=torch.long, device=dev)
+    buf_logp, buf_rew, buf_done, buf_val = (torch.zeros((num_steps, n), device=dev) for _ in range(4))
+
+    def as_dev(x):
+        return (x if torch.is_tensor(x) else torch.from_numpy(np.asarray(x))).to(dev).float()
+
+    next_obs = as_dev(envs.reset())
+    next_done = torch.zeros(n, device=dev)
+    ep_ret, finished = torch.zeros(n, device=dev), []
+    steps, t0, stats = 0, time.time(), {}
+    rollout_s = 0.0
+    for update in range(updates):
+        tr = time.time()
+        for t in range(num_steps):
+            buf_obs[t], buf_done[t] = next_obs, next_done
+            with torch.no_grad():
+                buf_mask[t] = as_dev(envs.get_action_mask())
+                a, logp, _, v = policy(net, next_obs, buf_mask[t], hw)
+            buf_act[t], buf_logp[t], buf_val[t] = a, logp, v
+            if api == "numpy":   # ppo_gridnet.py:475: host int64 actions, (N, H*W*7)
+                obs, rew, done, infos = envs.step(a.cpu().numpy().reshape(n, -1))
+                raw = torch.from_numpy(np.array([i["raw_rewards"] for i in infos])).to(dev)
+            else:
+                obs, rew, done, infos = envs.step(a)
+                raw = infos._raw
+            next_obs, buf_rew[t], next_done = as_dev(obs), as_dev(rew), as_dev(done)
+            ep_ret += (raw @ torch.as_tensor(envs.reward_weight, device=dev)).float()
+            if bool(next_done.any()):
+                finished += ep_ret[next_done.bool()].tolist()
+                ep_ret[next_done.bool()] = 0
+            steps += n
+        torch.cuda.synchronize(dev)
+        rollout_s += time.time() - tr
+        with torch.no_grad():   # GAE (gamma 0.99, lambda 0.95)
+            _, last_v = net(next_obs)
+            adv = torch.zeros_like(buf_rew)
+            gae = torch.zeros(n, device=dev)
+            for t in reversed(range(num_steps)):
+                nv, nd = (last_v, next_done) if t == num_steps - 1 else (buf_val[t + 1], buf_done[t + 1])
+                delta = buf_rew[t] + 0.99 * nv * (1 - nd) - buf_val[t]
+                gae = delta + 0.99 * 0.95 * (1 - nd) * gae
+                adv[t] = gae
+            ret = adv + buf_val
+        B = num_steps * n
+        flat = [x.reshape((B,) + x.shape[2:]) for x in (buf_obs, buf_mask, buf_act, buf_logp, adv, ret, buf_val)]
+        mb = max(1, B // minibatches)
+        for _ in range(epochs):
+            perm = torch.randperm(B, device=dev)
+            for s in range(0, B, mb):
+                idx = perm[s:s + mb]
+                o, m, a, lp0, ad, rt, v0 = (x[idx] for x in flat)
+                ad = (ad - ad.mean()) / (ad.std() + 1e-8)
+                _, lp, ent, v = policy(net, o, m, hw, action=a)
+                ratio = (lp - lp0).exp()
+                pg = torch.max(-ad * ratio, -ad * ratio.clamp(0.9, 1.1)).mean()
+                vc = v0 + (v - v0).clamp(-0.1, 0.1)
+                vl = 0.5 * torch.max((v - rt) ** 2, (vc - rt) ** 2).mean()
+                loss = pg - 0.01 * ent.mean() + 0.5 * vl
+                opt.zero_grad()
+                loss.backward()
+                nn.utils.clip_grad_norm_(net.parameters(), 0.5)
+                opt.step()
+        torch.cuda.synchronize(dev)
+        stats = {"update": update + 1, "global_step": steps, "sps": round(steps / (time.time() - t0), 1),
+                 "rollout_env_steps_per_s": round(steps / rollout_s, 1), "loss": float(loss.detach()), "policy_loss": float(pg.detach()),
+                 "value_loss": float(vl.detach()), "entropy": float(ent.detach().mean()), "episodes": len(finished)}
+        log(stats)
+    stats["engine_error_flags"] = envs.error_flags()
+    stats["finite"] = bool(np.isfinite([stats["loss"], stats["value_loss"], stats["entropy"]]).all())
+    envs.close()
+    return stats
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--num-selfplay-envs", type=int, default=2)
+    ap.add_argument("--num-bot-envs", type=int, default=0)
+    ap.add_argument("--partial-obs", action="store_true")
+    ap.add_argument("--num-steps", type=int, default=16)
+    ap.add_argument("--updates", type=int, default=2)
+    ap.add_argument("--minibatches", type=int, default=4)
+    ap.add_argument("--api", choices=["numpy", "tensor"], default="numpy")
+    a = ap.parse_args()
+    out = run(a.num_selfplay_envs, a.num_bot_envs, a.partial_obs, a.num_steps, a.updates, a.api, a.minibatches,
+              log=lambda s: print(json.dumps(s), flush=True))
+    print(json.dumps(out))
