@@ -1,7 +1,8 @@
 """Training-map catalogue: the same entries, in the same order, as
 /root/reference/gym_microrts/microrts_maps.py:1-20 (ALL16x16_MAPS).  Paths are
 relative to gym_microrts/microrts; the maps themselves are authored in this repo
-(scripts/author_maps.py) -- only some of the listed layouts exist so far."""
+(scripts/author_maps.py: the Java submodule holding the originals is absent, so
+every layout except basesWorkers16x16A's is an authored one, parity unpinned)."""
 
 _VARIANTS = ["A", "E", "I", "noResources", "melee:Mixed12", "B", "F", "J", "R20", "melee:Mixed8", "C", "G", "K",
              "TwoBasesBarracks", "D", "H", "L", "EightBasesWorkers"]

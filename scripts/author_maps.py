@@ -70,6 +70,36 @@ def main():
     write_map("16x16/TwoBasesBarracks16x16.xml", 16, 16,
               [R(0, 0), R(0, 1), R(15, 14), R(15, 15), B(0, 2, 2), ("Barracks", 0, 4, 2, 0, 4), B(1, 13, 13),
                ("Barracks", 1, 11, 13, 0, 4), W(0, 1, 1), W(1, 14, 14)])
+    # the rest of microrts_maps.ALL16x16_MAPS (authored, point-symmetric; parity unpinned for geometry)
+    def sym(units):   # add player 1's point-symmetric copy of player-0 / neutral units
+        out = []
+        for (t, p, x, y, r, hp) in units:
+            out.append((t, p, x, y, r, hp))
+            out.append((t, -1 if p < 0 else 1 - p, 15 - x, 15 - y, r, hp))
+        return out
+    variants = {   # base (x, y), worker (x, y), resource piles
+        "D": ((2, 3), (1, 3), [(0, 2), (0, 3)]), "E": ((3, 3), (2, 2), [(0, 0), (1, 0)]),
+        "F": ((2, 4), (1, 4), [(0, 5), (0, 6)]), "G": ((4, 2), (4, 1), [(5, 0), (6, 0)]),
+        "H": ((3, 2), (3, 1), [(0, 0), (0, 1), (1, 0)]), "I": ((2, 2), (2, 1), [(0, 3), (0, 4)]),
+        "J": ((5, 2), (5, 1), [(0, 0), (7, 0)]), "K": ((2, 5), (1, 5), [(0, 0), (0, 7)]),
+        "L": ((4, 4), (3, 3), [(0, 0), (0, 1), (1, 0), (1, 1)]),
+    }
+    for v, (b, wk, piles) in variants.items():
+        write_map(f"16x16/basesWorkers16x16{v}.xml", 16, 16,
+                  sym([R(x, y) for (x, y) in piles] + [B(0, *b), W(0, *wk)]))
+    write_map("16x16/basesWorkers16x16R20.xml", 16, 16, sym([R(0, 0, 20), R(0, 1, 20), B(0, 2, 2), W(0, 1, 1)]), res=(20, 20))
+    write_map("16x16/EightBasesWorkers16x16.xml", 16, 16,
+              sym([R(0, 0), R(0, 15), B(0, 2, 2), B(0, 2, 6), B(0, 6, 2), B(0, 2, 10), W(0, 1, 1), W(0, 3, 6), W(0, 6, 3),
+                   W(0, 3, 10)]))
+
+    def army(kinds):   # melee maps: two armies facing each other, no bases
+        units = []
+        for i, k in enumerate(kinds):
+            hp = {"Light": 4, "Heavy": 4, "Ranged": 1, "Worker": 1}[k]
+            units.append((k, 0, 4 + (i % 8), 3 + i // 8, 0, hp))
+        return sym(units)
+    write_map("16x16/melee16x16Mixed8.xml", 16, 16, army(["Light", "Heavy", "Ranged", "Worker"] * 2))
+    write_map("16x16/melee16x16Mixed12.xml", 16, 16, army(["Light", "Heavy", "Ranged", "Worker"] * 3))
     # 4x4 mask / reward test map
     write_map("4x4/baseTwoWorkers4x4.xml", 4, 4,
               [R(0, 0), R(3, 3), B(0, 1, 1), B(1, 2, 2), W(0, 1, 0), W(0, 0, 1), W(1, 2, 3), W(1, 3, 2)])

@@ -284,22 +284,20 @@ def test_device_sampler_ragged_rows(rows):
     np.testing.assert_array_equal(out.cpu().numpy(), sample_actions(m, 42, 7))
 
 
-def test_map_cycling_matches_oracle():
-    """cycle_maps (vec_env.py:1038-1056): finished games restart on the next map."""
+def _cycling(cyc, nsp, nbot, max_steps, steps):
     from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
     from gym_microrts import microrts_ai
     from oracle_py import sample_actions
 
-    cyc = ["maps/16x16/basesWorkers16x16A.xml", "maps/16x16/basesWorkers16x16B.xml", "maps/16x16/basesWorkers16x16C.xml"]
-    g = MicroRTSGridModeVecEnv(num_selfplay_envs=8, num_bot_envs=4, max_steps=60, ai2s=[microrts_ai.passiveAI] * 4,
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=max_steps, ai2s=[microrts_ai.passiveAI] * nbot,
                                map_paths=[cyc[0]], cycle_maps=cyc, reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]))
-    table = [os.path.join(MAPS, p) for p in cyc]
-    o = make_oracle(8, 4, None, 60, maps=table)
+    table = [os.path.join(MAPS, p) for p in dict.fromkeys(cyc)]
+    o = make_oracle(nsp, nbot, None, max_steps, maps=table)
     np.testing.assert_array_equal(g.reset(), o.reset())
     from itertools import cycle
 
-    nxt = cycle(range(3))
-    for s in range(200):
+    nxt = cycle([table.index(os.path.join(MAPS, p)) for p in cyc])
+    for s in range(steps):
         mo = o.get_action_mask()
         np.testing.assert_array_equal(g.get_action_mask(), mo)
         a = sample_actions(mo, 99, s)
@@ -308,12 +306,27 @@ def test_map_cycling_matches_oracle():
         np.testing.assert_array_equal(rg, ro)
         np.testing.assert_array_equal(dg, do)
         for e in np.nonzero(do)[0]:
-            if e < 8 and e % 2:
+            if e < nsp and e % 2:
                 continue
-            game = e // 2 if e < 8 else 4 + (e - 8)
+            game = e // 2 if e < nsp else nsp // 2 + (e - nsp)
             o.reset_game(game, next(nxt))
         oo = o.encode(o.raw_obs())
         np.testing.assert_array_equal(og, oo, err_msg=f"step {s}")
+    assert g.error_flags() == 0
+
+
+def test_map_cycling_matches_oracle():
+    """cycle_maps (vec_env.py:1038-1056): finished games restart on the next map."""
+    _cycling(["maps/16x16/basesWorkers16x16A.xml", "maps/16x16/basesWorkers16x16B.xml", "maps/16x16/basesWorkers16x16C.xml"],
+             8, 4, 60, 200)
+
+
+def test_all16x16_maps_cycling():
+    """ppo_gridnet's training-map catalogue (microrts_maps.ALL16x16_MAPS, authored
+    layouts incl. melee and eight-base maps) cycled through every game."""
+    from gym_microrts.microrts_maps import ALL16x16_MAPS
+
+    _cycling(ALL16x16_MAPS, 24, 6, 70, 400)
 
 
 def test_no_invariant_violation_long_run():
