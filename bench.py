@@ -262,33 +262,49 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def cpu_baseline(seconds, envs=512):
+def cpu_baseline(seconds, envs=512, one_core_seconds=6.0):
     """The oracle (C restatement, OpenMP over games) on a bounded sample of the
-    same workload: 16x16 basesWorkers selfplay, random masked actions."""
+    same workload: 16x16 basesWorkers selfplay, random masked actions; all host
+    cores, plus a 1-core sample in a child process (OMP_NUM_THREADS=1)."""
+    import subprocess
+
+    res = cpu_sample(seconds, envs)
+    if one_core_seconds > 0:
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-sample", str(one_core_seconds)], env=env,
+                             capture_output=True, text=True, timeout=120)
+        one = json.loads(out.stdout.strip().splitlines()[-1])
+        res["value_1core"] = one["value"]
+        res["sample_1core"] = one["sample"]
+    return res
+
+
+def cpu_sample(seconds, envs=512):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    from oracle_py import OracleVecEnv, sample_actions
+    from oracle_py import OracleVecEnv
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     path = os.path.join(REPO, "microrts-py_amd", "gym_microrts", "microrts", MAP)
     o = OracleVecEnv(envs, 0, [path], max_steps=2000)
     o.reset()
-    for s in range(5):
-        o.step(sample_actions(o.get_action_mask(), 1, s))
+    o.bench_steps(5, 1, 0)
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds or steps < 5:
-        m = o.get_action_mask()
-        o.step(sample_actions(m, 1, 5 + steps))
-        steps += 1
+        o.bench_steps(5, 1, 5 + steps)
+        steps += 5
     dt = time.perf_counter() - t0
     o.close()
     return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/libmrts_oracle.so, {envs} selfplay envs x {steps} steps ({dt:.1f} s), 16x16 basesWorkers, "
-                      f"masks + sampler + step + obs encode, OMP_NUM_THREADS={threads}"}
+            "sample": f"oracle/libmrts_oracle.so ovec_bench_steps, {envs} selfplay envs x {steps} steps ({dt:.1f} s), "
+                      f"16x16 basesWorkers, masks + sampler + step + obs encode in C, OpenMP over envs, OMP_NUM_THREADS={threads}"}
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-sample":   # child of cpu_baseline (no GPU use)
+        print(json.dumps(cpu_sample(float(sys.argv[2]), envs=64)), flush=True)
+        return
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -899,8 +899,9 @@ void ovec_encode_obs(const int32_t *raw, int n, int h, int w, int partial_obs, i
     for (int i = 0; i < P_raw; i++) prefix[i + 1] = prefix[i] + nplanes[i];
     int P = prefix[P_raw];
     int HW = h * w;
-    memset(out, 0, sizeof(int32_t) * (size_t)n * HW * P);
-    for (int e = 0; e < n; e++)
+#pragma omp parallel for schedule(static)
+    for (int e = 0; e < n; e++) {
+        memset(out + (size_t)e * HW * P, 0, sizeof(int32_t) * (size_t)HW * P);
         for (int c = 0; c < HW; c++)
             for (int k = 0; k < P_raw; k++) {
                 int val = raw[((size_t)e * P_raw + k) * HW + c];
@@ -908,6 +909,7 @@ void ovec_encode_obs(const int32_t *raw, int n, int h, int w, int partial_obs, i
                 if (val > nplanes[k] - 1) val = nplanes[k] - 1;
                 out[((size_t)e * HW + c) * P + prefix[k] + val] = 1;
             }
+    }
 }
 
 int ovec_game_time(const OVec *v, int game) { return v->gs[game].time; }
@@ -955,36 +957,60 @@ static void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
     }
 }
 
-void ovec_sample_actions(const int32_t *m78, int n, int hw, uint64_t seed, uint32_t step, int64_t *act) {
+/* one (env, cell) row of the masked sampler: m = the 78 channels */
+static void sample_row(const int32_t *m, int e, int c, uint64_t seed, uint32_t step, int64_t *out) {
     static const int seg_off[7] = {0, 6, 10, 14, 18, 22, 29};
     static const int seg_len[7] = {6, 4, 4, 4, 4, 7, 49};
-#pragma omp parallel for schedule(static)
-    for (int e = 0; e < n; e++) {
-        for (int c = 0; c < hw; c++) {
-            const int32_t *m = m78 + ((size_t)e * hw + c) * 78;
-            uint32_t r[8];
-            for (int h = 0; h < 2; h++) {
-                uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
-                philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-                for (int j = 0; j < 4; j++) r[4 * h + j] = ctr[j];
-            }
-            for (int k = 0; k < 7; k++) {
-                int nvalid = 0;
-                for (int j = 0; j < seg_len[k]; j++) nvalid += m[seg_off[k] + j] != 0;
-                int pick;
-                if (nvalid == 0) {
-                    pick = (int)(((uint64_t)r[k] * (uint32_t)seg_len[k]) >> 32);
-                } else {
-                    int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
-                    pick = 0;
-                    for (int j = 0; j < seg_len[k]; j++)
-                        if (m[seg_off[k] + j]) {
-                            if (t == 0) { pick = j; break; }
-                            t--;
-                        }
+    uint32_t r[8];
+    for (int h = 0; h < 2; h++) {
+        uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
+        philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        for (int j = 0; j < 4; j++) r[4 * h + j] = ctr[j];
+    }
+    for (int k = 0; k < 7; k++) {
+        int nvalid = 0;
+        for (int j = 0; j < seg_len[k]; j++) nvalid += m[seg_off[k] + j] != 0;
+        int pick;
+        if (nvalid == 0) {
+            pick = (int)(((uint64_t)r[k] * (uint32_t)seg_len[k]) >> 32);
+        } else {
+            int t = (int)(((uint64_t)r[k] * (uint32_t)nvalid) >> 32);
+            pick = 0;
+            for (int j = 0; j < seg_len[k]; j++)
+                if (m[seg_off[k] + j]) {
+                    if (t == 0) { pick = j; break; }
+                    t--;
                 }
-                act[((size_t)e * hw + c) * 7 + k] = pick;
-            }
         }
+        out[k] = pick;
+    }
+}
+
+void ovec_sample_actions(const int32_t *m78, int n, int hw, uint64_t seed, uint32_t step, int64_t *act) {
+#pragma omp parallel for schedule(static)
+    for (int e = 0; e < n; e++)
+        for (int c = 0; c < hw; c++)
+            sample_row(m78 + ((size_t)e * hw + c) * 78, e, c, seed, step, act + ((size_t)e * hw + c) * 7);
+}
+
+/* The bench's CPU baseline: `steps` env-steps of every env -- getMasks, the
+ * masked sampler on channels 1..78, gameStep, raw obs + one-hot encode -- with
+ * OpenMP over games / envs and no Python between the stages.  Buffers are the
+ * caller's: masks79 [N][HW][79], act [N][HW][7], src [N][HW], reward [N][6],
+ * done [N][6], obs [N][HW][P]. */
+void ovec_bench_steps(OVec *v, int steps, uint64_t seed, uint32_t step0, int32_t *masks79, int64_t *act, int32_t *src,
+                      double *reward, uint8_t *done, int32_t *obs) {
+    const int n = v->nenvs, hw = v->W * v->H;
+    for (int s = 0; s < steps; s++) {
+        ovec_get_masks(v, masks79);
+#pragma omp parallel for schedule(static)
+        for (int e = 0; e < n; e++)
+            for (int c = 0; c < hw; c++) {
+                const int32_t *m = masks79 + ((size_t)e * hw + c) * 79;
+                src[(size_t)e * hw + c] = m[0];
+                sample_row(m + 1, e, c, seed, step0 + (uint32_t)s, act + ((size_t)e * hw + c) * 7);
+            }
+        ovec_step(v, act, src, reward, done);
+        ovec_encode_obs(v->raw, n, v->H, v->W, v->partial_obs, obs);
     }
 }

@@ -86,6 +86,11 @@ void ovec_dump_cells(const OVec *v, int game, int32_t *out);
 void ovec_sample_actions(const int32_t *masks78, int n, int hw, uint64_t seed,
                          uint32_t step, int64_t *actions);
 
+/* CPU baseline of bench.py: `steps` whole env-steps (masks, sampler, step,
+ * obs encode) with OpenMP over envs; see mrts_oracle.c. */
+void ovec_bench_steps(OVec *v, int steps, uint64_t seed, uint32_t step0, int32_t *masks79, int64_t *act, int32_t *src,
+                      double *reward, uint8_t *done, int32_t *obs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,6 +49,7 @@ def lib():
         L.ovec_game_resources.argtypes = [P, ctypes.c_int, P]
         L.ovec_dump_cells.argtypes = [P, ctypes.c_int, P]
         L.ovec_sample_actions.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P]
+        L.ovec_bench_steps.argtypes = [P, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -173,6 +174,20 @@ class OracleVecEnv:
         r = np.zeros(2, np.int32)
         lib().ovec_game_resources(self._h, g, ptr(r))
         return r
+
+    def bench_steps(self, steps, seed, step0):
+        """`steps` whole env-steps in C (masks, sampler, step, encode; OpenMP):
+        the bench's CPU baseline.  Returns the last (obs, raw rewards, dones)."""
+        n, hw = self.num_envs, self.height * self.width
+        if getattr(self, "_bench_bufs", None) is None:
+            P = 31 if self.partial_obs else 29
+            self._bench_bufs = (np.zeros((n, hw, 79), np.int32), np.zeros((n, hw, 7), np.int64), np.zeros((n, hw), np.int32),
+                                np.zeros((n, 6), np.float64), np.zeros((n, 6), np.uint8),
+                                np.zeros((n, self.height, self.width, P), np.int32))
+        m, a, src, rew, done, obs = self._bench_bufs
+        lib().ovec_bench_steps(self._h, steps, ctypes.c_uint64(seed), ctypes.c_uint32(step0), ptr(m), ptr(a), ptr(src),
+                               ptr(rew), ptr(done), ptr(obs))
+        return obs, rew, done.astype(bool)
 
     def dump_cells(self, g):
         out = np.zeros((self.height * self.width, 8), np.int32)

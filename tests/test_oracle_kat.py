@@ -136,3 +136,19 @@ def test_partial_obs_rollout_invariants():
         # own units are never hidden
         own = fo[..., 11] == 1
         np.testing.assert_array_equal(obs[..., :29][own], fo[own])
+
+
+def test_bench_loop_equals_python_loop():
+    """ovec_bench_steps (bench.py's CPU baseline) == get_action_mask + sample_actions
+    + step + encode driven from Python, step for step."""
+    path = os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml")
+    a, b = OracleVecEnv(16, 0, [path], max_steps=120), OracleVecEnv(16, 0, [path], max_steps=120)
+    a.reset()
+    b.reset()
+    for s in range(300):
+        obs_a, rew_a, done_a = a.bench_steps(1, 7, s)
+        m = b.get_action_mask()
+        obs_b, _, done_b, infos = b.step(sample_actions(m, 7, s))
+        np.testing.assert_array_equal(obs_a, obs_b, err_msg=f"step {s}")
+        np.testing.assert_array_equal(rew_a, np.array([i["raw_rewards"] for i in infos]))
+        np.testing.assert_array_equal(done_a[:, 0], done_b)
