@@ -654,6 +654,9 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
     Lds L = carve(smem, HW, p.W, NT);
     const Grid gd{p.W, p.H, HW};
 #ifdef MRTS_EXP_FILL   // kernel-variant experiments only: zeros over one launch's output bytes, no loads
+#ifndef MRTS_EXP_FILL_SPLIT
+#define MRTS_EXP_FILL_SPLIT 1
+#endif
     {
         const v4i z = {0, 0, 0, 0};
         if (MRTS_EXP_FILL == 1) {   // per game: its envs' obs + mask rows (k_step's pattern)
@@ -662,6 +665,14 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
             for (int k = threadIdx.x; k < G.nviews * HW * P / 4; k += NT) o[k] = z;
             v4i* m = reinterpret_cast<v4i*>(p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH);
             for (int k = threadIdx.x; k < G.nviews * HW * MRTS_MASK_CH / 4; k += NT) m[k] = z;
+        } else if (MRTS_EXP_FILL == 3) {   // each game's rows split over MRTS_EXP_FILL_SPLIT blocks
+            const int part = blockIdx.x % MRTS_EXP_FILL_SPLIT;
+            const Game G = game_of(p, blockIdx.x / MRTS_EXP_FILL_SPLIT);
+            const int no = G.nviews * HW * P / 4, nm = G.nviews * HW * MRTS_MASK_CH / 4;
+            v4i* o = reinterpret_cast<v4i*>(reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P);
+            for (int k = part * no / MRTS_EXP_FILL_SPLIT + threadIdx.x; k < (part + 1) * no / MRTS_EXP_FILL_SPLIT; k += NT) o[k] = z;
+            v4i* m = reinterpret_cast<v4i*>(p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH);
+            for (int k = part * nm / MRTS_EXP_FILL_SPLIT + threadIdx.x; k < (part + 1) * nm / MRTS_EXP_FILL_SPLIT; k += NT) m[k] = z;
         } else {                    // grid-stride over both arrays (a fill kernel's pattern)
             const long long N = p.nsp + (p.G - p.nsp_games), st = (long long)gridDim.x * NT;
             v4i* o = reinterpret_cast<v4i*>(p.obs);
@@ -1270,6 +1281,9 @@ static int resident_blocks(const void* kernel, int NT, size_t sh) {
 template <typename K>
 static void launch_step(K kernel, int NT, size_t sh, hipStream_t s, const EngineParams& p) {
     int grid = p.G;
+#ifdef MRTS_EXP_FILL_SPLIT
+    grid *= MRTS_EXP_FILL_SPLIT;
+#endif
 #ifdef MRTS_STEP_PERSISTENT
     const int cap = resident_blocks(reinterpret_cast<const void*>(kernel), NT, sh);
     if (cap > 0) grid = std::min(grid, cap);
