@@ -120,6 +120,58 @@ __device__ int cell_of_uid(const BS& S, const BL& L, int uid) {
     return -1;
 }
 
+// ---- wave-parallel scans of the unit list (results identical in every lane) ----
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long k) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(k, o);
+        k = v < k ? v : k;
+    }
+    return k;
+}
+// The first unit in pgs.units order (a serial `d < best` scan) among those
+// `want` selects minimising the Manhattan distance to (x, y): min over
+// (distance, list index) across the lanes.  -1 if none; *dist = that distance.
+template <typename F>
+__device__ __forceinline__ int closest_unit(const BS& S, const BL& L, int x, int y, F want, int* dist = nullptr) {
+    unsigned long long key = ~0ull;
+    for (int k = threadIdx.x; k < S.n; k += BT) {
+        const int c = L.ucell[k];
+        if (!want(c)) continue;
+        const unsigned d = (unsigned)(iabs(c % S.W - x) + iabs(c / S.W - y));
+        const unsigned long long kk = ((unsigned long long)d << 32) | (unsigned)k;
+        key = kk < key ? kk : key;
+    }
+    key = wave_min_u64(key);
+    if (key == ~0ull) return -1;
+    if (dist) *dist = (int)(key >> 32);
+    return L.ucell[(int)(key & 0xFFFFFFFFu)];
+}
+// number of units `want` selects
+template <typename F>
+__device__ __forceinline__ int count_where(const BS& S, const BL& L, F want) {
+    int n = 0;
+    for (int base = 0; base < S.n; base += BT) {
+        const int k = base + threadIdx.x;
+        n += __popcll(__ballot(k < S.n && want(L.ucell[k])));
+    }
+    return n;
+}
+// the idx-th unit (pgs.units order) `want` selects, -1 if fewer
+template <typename F>
+__device__ __forceinline__ int nth_where(const BS& S, const BL& L, int idx, F want) {
+    for (int base = 0; base < S.n; base += BT) {
+        const int k = base + threadIdx.x;
+        unsigned long long m = __ballot(k < S.n && want(L.ucell[k]));
+        const int cnt = __popcll(m);
+        if (idx < cnt) {
+            for (int t = 0; t < idx; t++) m &= m - 1ull;
+            return L.ucell[base + __builtin_ctzll(m)];
+        }
+        idx -= cnt;
+    }
+    return -1;
+}
+
 // ---- ResourceUsage ----------------------------------------------------------
 struct RU {
     int pos;    // unchecked x + y*W + offset, or INT_MIN for none
@@ -178,6 +230,9 @@ __device__ void pa_add(BS& S, const BL& L, int c, int code) {
 // the target) over free cells; the first layer that touches a free neighbour
 // of the start decides the move, ties UP, RIGHT, DOWN, LEFT.  -1 = null.
 __device__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
+#ifdef MRTS_EXP_NOPF   // kernel-variant experiments only: path finding skipped (behaviour changes)
+    return -1;
+#endif
     const int lane = threadIdx.x, sx = sc % S.W, sy = sc / S.W, r2 = range * range;
     if ((sx - tx) * (sx - tx) + (sy - ty) * (sy - ty) <= r2) return -1;
     const uint32_t rowmask = S.W == 32 ? 0xFFFFFFFFu : ((1u << S.W) - 1u);
@@ -212,9 +267,12 @@ __device__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
 }
 
 // ---- abstract actions ----------------------------------------------------------
-__device__ int find_aa(const BS& S, const BL& L, int uid) {
-    for (int k = 0; k < S.naa; k++)
-        if (L.aa[2 * k].x == uid) return k;
+__device__ int find_aa(const BS& S, const BL& L, int uid) {   // first entry of the unit, lane-parallel
+    for (int base = 0; base < S.naa; base += BT) {
+        const int k = base + threadIdx.x;
+        const unsigned long long m = __ballot(k < S.naa && L.aa[2 * k].x == uid);
+        if (m) return base + __builtin_ctzll(m);
+    }
     return -1;
 }
 __device__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   // actions.put(u, aa)
@@ -256,19 +314,11 @@ __device__ int adj_dir(int ux, int uy, int x, int y) {
 }
 
 __device__ int train_score(const BS& S, const BL& L, int x, int y, int type, int player) {   // Train.score
-    int dist = 0;
-    bool first = true;
-    for (int k = 0; k < S.n; k++) {
-        const int c = L.ucell[k];
+    int dist = 0;   // stays 0 when nothing qualifies
+    closest_unit(S, L, x, y, [&](int c) {
         const uint32_t o = L.unit[c];
-        const bool want = ut_can_harvest(type) ? u_type(o) == RESOURCE : (u_owner(o) >= 0 && u_owner(o) != player);
-        if (!want) continue;
-        int d = iabs(c % S.W - x) + iabs(c / S.W - y);
-        if (first || d < dist) {
-            dist = d;
-            first = false;
-        }
-    }
+        return ut_can_harvest(type) ? u_type(o) == RESOURCE : (u_owner(o) >= 0 && u_owner(o) != player);
+    }, &dist);
     return -dist;
 }
 
@@ -385,35 +435,18 @@ __device__ void translate_actions(BS& S, const BL& L) {
 
 // ---- behaviours ------------------------------------------------------------------
 __device__ int closest_enemy(const BS& S, const BL& L, int cu) {
-    const int me = u_owner(L.unit[cu]), ux = cu % S.W, uy = cu / S.W;
-    int best = -1, bd = 0;
-    for (int k = 0; k < S.n; k++) {
-        const int c = L.ucell[k];
+    const int me = u_owner(L.unit[cu]);
+    return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
         const int o = u_owner(L.unit[c]);
-        if (o < 0 || o == me) continue;
-        int d = iabs(c % S.W - ux) + iabs(c / S.W - uy);
-        if (best < 0 || d < bd) {
-            best = c;
-            bd = d;
-        }
-    }
-    return best;
+        return o >= 0 && o != me;
+    });
 }
 __device__ int closest_of(const BS& S, const BL& L, int cu, bool want_resource) {
-    const int me = u_owner(L.unit[cu]), ux = cu % S.W, uy = cu / S.W;
-    int best = -1, bd = 0;
-    for (int k = 0; k < S.n; k++) {
-        const int c = L.ucell[k];
+    const int me = u_owner(L.unit[cu]);
+    return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
         const uint32_t o = L.unit[c];
-        const bool ok = want_resource ? u_type(o) == RESOURCE : (ut_is_stockpile(u_type(o)) && u_owner(o) == me);
-        if (!ok) continue;
-        int d = iabs(c % S.W - ux) + iabs(c / S.W - uy);
-        if (best < 0 || d < bd) {
-            best = c;
-            bd = d;
-        }
-    }
-    return best;
+        return want_resource ? u_type(o) == RESOURCE : (ut_is_stockpile(u_type(o)) && u_owner(o) == me);
+    });
 }
 
 // meleeUnitBehavior (+ PO* exploration: nearest cell the player cannot observe)
@@ -488,13 +521,10 @@ __device__ void build_if_not_already(BS& S, const BL& L, int cu, int type, int* 
 }
 
 __device__ int count_units(const BS& S, const BL& L, int type, bool own) {
-    int n = 0;
-    for (int k = 0; k < S.n; k++) {
-        const uint32_t o = L.unit[L.ucell[k]];
-        if (u_type(o) != type) continue;
-        n += own ? (u_owner(o) == S.player) : (u_owner(o) >= 0 && u_owner(o) != S.player);
-    }
-    return n;
+    return count_where(S, L, [&](int c) {
+        const uint32_t o = L.unit[c];
+        return u_type(o) == type && (own ? u_owner(o) == S.player : (u_owner(o) >= 0 && u_owner(o) != S.player));
+    });
 }
 
 // WorkerRush / LightRush / HeavyRush / RangedRush (+ PO*), and coacAI
@@ -531,25 +561,14 @@ __device__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac
         melee_behavior(S, L, c, po);
     }
     // workers, busy ones included (the list is the tail of the unit list walk)
-    int nf = 0;
-    for (int k = 0; k < S.n; k++) {
-        const uint32_t u = L.unit[L.ucell[k]];
-        nf += ut_can_harvest(u_type(u)) && u_owner(u) == p;
-    }
+    auto own_worker = [&](int c) {
+        const uint32_t u = L.unit[c];
+        return ut_can_harvest(u_type(u)) && u_owner(u) == p;
+    };
+    const int nf = count_where(S, L, own_worker);
     if (nf > 0) {
         int reserved[4], nres = 0, used = 0, head = 0;   // head: workers taken off the free list
-        auto worker = [&](int idx) {                      // idx-th own worker in pgs.units order
-            int seen = 0;
-            for (int k = 0; k < S.n; k++) {
-                const int c = L.ucell[k];
-                const uint32_t u = L.unit[c];
-                if (ut_can_harvest(u_type(u)) && u_owner(u) == p) {
-                    if (seen == idx) return c;
-                    seen++;
-                }
-            }
-            return -1;
-        };
+        auto worker = [&](int idx) { return nth_where(S, L, idx, own_worker); };   // idx-th own worker, pgs.units order
         if (nbases == 0 && head < nf && res >= ut_cost(BASE) + used) {
             build_if_not_already(S, L, worker(head++), BASE, reserved, nres);
             used += ut_cost(BASE);
@@ -667,7 +686,10 @@ __device__ void random_biased_get_action(BS& S, const BL& L) {
 }
 
 // ---- the kernel ------------------------------------------------------------------------
-__global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
+#ifndef MRTS_BOT_MIN_WAVES
+#define MRTS_BOT_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // blockIdx.y = the bot's player: 1 = ai2 (every bot env), 0 = ai1 of a
     // bot-vs-bot game (MicroRTSBotVecEnv); both see the same pre-issue state
@@ -711,8 +733,9 @@ __global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
     for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
     if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     __syncthreads();
-    // cells observable by the bot's player (PartiallyObservableGameState)
-    for (int c = lane; c < HW; c += BT) {
+    // cells observable by the bot's player (PartiallyObservableGameState);
+    // read only under partial observability (hidden units, PO* exploration)
+    for (int c = lane; S.partial && c < HW; c += BT) {
         const uint32_t u = L.unit[c];
         if (u == 0 || u_owner(u) != S.player) continue;
         const int r = ut_sight(u_type(u)), x = c % W, y = c / W;

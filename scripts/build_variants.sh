@@ -7,9 +7,8 @@ C=microrts-py_amd/csrc
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Iinclude -I$C -shared"
 S="$C/mrts_engine.hip $C/mrts_bots.hip $C/mrts_capi.cpp"
 build() { name=$1; shift; /opt/rocm/bin/hipcc $F "$@" -o scripts/_exp/lib_$name.so $S & }
-build fill1 -DMRTS_EXP_FILL=1
+build base
 
-build split4 -DMRTS_EXP_FILL=3 -DMRTS_EXP_FILL_SPLIT=4
-build split16 -DMRTS_EXP_FILL=3 -DMRTS_EXP_FILL_SPLIT=16
+
 wait
 ls -la scripts/_exp
