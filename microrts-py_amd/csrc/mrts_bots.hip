@@ -30,6 +30,15 @@ namespace mrts {
 
 constexpr int BT = 64;   // one wavefront per bot game
 
+#ifdef MRTS_EXP_STAMPS   // kernel-variant experiments only: per-phase s_memtime stamps of k_bot
+constexpr int NSTAMP = 8, MAXSTAMPB = 16384;
+__device__ unsigned long long mrts_bot_stamps[MAXSTAMPB][NSTAMP];
+#define BOT_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < MAXSTAMPB && blockIdx.y == gridDim.y - 1) \
+    mrts_bot_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BOT_STAMP(i) do { } while (0)
+#endif
+
 enum { AA_NONE = 0, AA_MOVE, AA_HARVEST, AA_ATTACK, AA_TRAIN, AA_BUILD };
 
 // abstract-action entry = 2 x int4 (LinkedHashMap<Unit, AbstractAction> order):
@@ -434,7 +443,10 @@ __device__ void translate_actions(BS& S, const BL& L) {
 }
 
 // ---- behaviours ------------------------------------------------------------------
-__device__ int closest_enemy(const BS& S, const BL& L, int cu) {
+// closest enemy of the unit at cu: precomputed for every unit in k_bot before
+// the behaviours (L.pa[cell]) for the rush family; wave-parallel scan otherwise
+__device__ int closest_enemy(const BS& S, const BL& L, int cu, bool table = true) {
+    if (table) return L.pa[cu];
     const int me = u_owner(L.unit[cu]);
     return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
         const int o = u_owner(L.unit[c]);
@@ -592,6 +604,7 @@ __device__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac
             }
         }
     }
+    BOT_STAMP(5);
     translate_actions(S, L);
 }
 
@@ -705,6 +718,7 @@ __global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) 
         return;
     }
     BL L = bot_carve(smem, HW, W);
+    BOT_STAMP(0);
     int4* const aa_g = p.aa + ((size_t)b * 2 + player) * HW * 2;
     int32_t* const pa_g = p.botpa + ((size_t)b * 2 + player) * HW;
     S.W = W;
@@ -733,6 +747,7 @@ __global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) 
     for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
     if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     __syncthreads();
+    BOT_STAMP(1);
     // cells observable by the bot's player (PartiallyObservableGameState);
     // read only under partial observability (hidden units, PO* exploration)
     for (int c = lane; S.partial && c < HW; c += BT) {
@@ -759,6 +774,7 @@ __global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) 
         __syncthreads();
     }
     // pending reservations of the visible units (isUnitActionAllowed)
+    BOT_STAMP(2);
     for (int c = lane; c < HW; c += BT) {
         const uint32_t a = L.act[c];
         if (a == 0) continue;
@@ -778,25 +794,70 @@ __global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) 
         n += __popcll(m);
     }
     __syncthreads();
-    for (int i = lane; i < n; i += BT) {
-        const int c = L.pa[i], u = L.uid[c];
+    if (n <= BT) {   // rank by uid with the uids in registers (one per lane)
+        const int c = lane < n ? L.pa[lane] : 0, u = lane < n ? L.uid[c] : 0x7fffffff;
         int r = 0;
-        for (int j = 0; j < n; j++) r += L.uid[L.pa[j]] < u;
-        L.ucell[r] = c;
-        L.uuid[r] = u;
+        for (int j = 0; j < n; j++) r += __shfl(u, j) < u;
+        if (lane < n) {
+            L.ucell[r] = c;
+            L.uuid[r] = u;
+        }
+    } else {
+        for (int i = lane; i < n; i += BT) {
+            const int c = L.pa[i], u = L.uid[c];
+            int r = 0;
+            for (int j = 0; j < n; j++) r += L.uid[L.pa[j]] < u;
+            L.ucell[r] = c;
+            L.uuid[r] = u;
+        }
     }
     __syncthreads();
     S.n = n;
+    BOT_STAMP(3);
     S.pend_res[0] = L.sc[0];
     S.pend_res[1] = L.sc[1];
-    // lane y: free cells of row y
-    S.frow = 0;
+    // lane y: free cells of row y, from one ballot per 64 cells (staged in L.pa,
+    // free until the PlayerAction is built)
     S.rurow = 0;
-    if (lane < p.H)
-        for (int x = 0; x < W; x++) {
-            const int c = lane * W + x;
-            if (!L.wall[c] && L.unit[c] == 0) S.frow |= 1u << x;
+    {
+        uint32_t* fw = reinterpret_cast<uint32_t*>(L.pa);
+        const int nwords = (HW + 63) / 64 * 2;
+        for (int base = 0; base < HW; base += BT) {
+            const int c = base + lane;
+            const unsigned long long m = __ballot(c < HW && !L.wall[c] && L.unit[c] == 0);
+            if (lane == 0) {
+                fw[base / 32] = (uint32_t)m;
+                fw[base / 32 + 1] = (uint32_t)(m >> 32);
+            }
         }
+        if (lane == 0) fw[nwords] = 0u;   // the row window's upper word past the last cell
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        S.frow = 0;
+        if (lane < p.H) {
+            const int o = lane * W, q = o >> 5;
+            const uint64_t win = ((uint64_t)fw[q + 1] << 32) | fw[q];
+            S.frow = (uint32_t)(win >> (o & 31)) & (W == 32 ? 0xFFFFFFFFu : ((1u << W) - 1u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    // the closest enemy of every unit (the scan closest_enemy would do, all
+    // units at once; the state is fixed during getAction): L.pa[cell], staged
+    // like the rows above (-1 = none)
+    for (int k = lane; S.ai != MRTS_AI_RANDOM_BIASED && k < n; k += BT) {
+        const int cu = L.ucell[k], me = u_owner(L.unit[cu]), ux = cu % W, uy = cu / W;
+        unsigned long long key = ~0ull;
+        for (int j = 0; j < n; j++) {
+            const int c = L.ucell[j];
+            const int o = u_owner(L.unit[c]);
+            if (o < 0 || o == me) continue;
+            const unsigned d = (unsigned)(iabs(c % W - ux) + iabs(c / W - uy));
+            const unsigned long long kk = ((unsigned long long)d << 32) | (unsigned)j;
+            key = kk < key ? kk : key;
+        }
+        L.pa[cu] = key == ~0ull ? -1 : L.ucell[(int)(key & 0xFFFFFFFFu)];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    BOT_STAMP(4);
     switch (S.ai) {
     case MRTS_AI_WORKER_RUSH: rush_get_action(S, L, WORKER, false, false); break;
     case MRTS_AI_LIGHT_RUSH: rush_get_action(S, L, LIGHT, false, false); break;
@@ -809,6 +870,7 @@ __global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) 
     default: break;
     }
     __syncthreads();
+    BOT_STAMP(6);
     for (int i = lane; i < S.npa; i += BT) pa_g[i] = L.pa[i];
     for (int i = lane; i < 2 * S.naa; i += BT) aa_g[i] = L.aa[i];
     if (lane0()) {
@@ -828,4 +890,10 @@ hipError_t mrts_engine_bots(const EngineParams* p, hipStream_t s) {
     return hipGetLastError();
 }
 size_t mrts_engine_bot_lds_bytes(int HW, int W) { return mrts::bot_lds_bytes(HW, W); }
+#ifdef MRTS_EXP_STAMPS
+int mrts_exp_bot_stamps(unsigned long long* out, int nblocks) {   // experiment builds only
+    const int n = nblocks < mrts::MAXSTAMPB ? nblocks : mrts::MAXSTAMPB;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mrts::mrts_bot_stamps), sizeof(unsigned long long) * mrts::NSTAMP * n) ? -1 : n;
+}
+#endif
 }
