@@ -9,6 +9,5 @@ S="$C/mrts_engine.hip $C/mrts_bots.hip $C/mrts_capi.cpp"
 build() { name=$1; shift; /opt/rocm/bin/hipcc $F "$@" -o scripts/_exp/lib_$name.so $S & }
 build base
 
-
 wait
 ls -la scripts/_exp
