@@ -8,6 +8,10 @@ this image, so a minimal stand-in with the attributes the drivers read
 import numpy as np
 
 try:  # pragma: no cover - depends on the environment
+    import gym as _gym
+
+    if getattr(_gym, "__microrts_compat__", False):  # our own stand-in (compat/gym) re-exports this module
+        raise ImportError("gym stand-in")
     from gym.spaces import Box, Discrete, MultiDiscrete  # noqa: F401
 except Exception:  # gym absent
 
