@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true")
     ap.add_argument("--event-every", type=int, default=8,
                     help="record per-launch HIP events on every N-th step of the timed region")
+    ap.add_argument("--bot-lookahead", action="store_true",
+                    help="run the next tick's k_bot on a side stream right after each step (mrts_set_bot_lookahead)")
     ap.add_argument("--no-eager-masks", action="store_true",
                     help="get_action_mask() launches k_masks instead of k_step writing the next tick's masks")
     ap.add_argument("--sampler", default="src", choices=["src", "dense"],
@@ -194,7 +196,7 @@ def run_gpu(args, rank, world, local_rank):
     env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
                                  ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
                                  reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, return_tensors=True,
-                                 eager_masks=not args.no_eager_masks)
+                                 eager_masks=not args.no_eager_masks, bot_lookahead=args.bot_lookahead)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
     lib = _native.lib()

@@ -15,7 +15,8 @@ BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "POWorkerRush
         "PORangedRush"]
 
 
-def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=2000, mode="masked", return_tensors=False):
+def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=2000, mode="masked", return_tensors=False,
+             bot_lookahead=False):
     import torch
 
     from gym_microrts import microrts_ai
@@ -26,7 +27,7 @@ def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=200
     g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=len(ais), max_steps=max_steps,
                                ai2s=[getattr(microrts_ai, a) for a in ais], map_paths=[map_path], reward_weight=w,
                                partial_obs=partial_obs, return_tensors=return_tensors,
-                               obs_dtype=torch.int32 if return_tensors else None)
+                               obs_dtype=torch.int32 if return_tensors else None, bot_lookahead=bot_lookahead)
     o = OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais,
                      partial_obs=partial_obs, reward_weight=w)
     cpu = (lambda t: t.cpu().numpy()) if return_tensors else np.asarray
@@ -150,3 +151,39 @@ def test_mixed_map_buckets_match_oracle():
             np.testing.assert_array_equal(obs[k].cpu().numpy(), oo, err_msg=f"bucket {k} step {s}")
             np.testing.assert_array_equal(done[k].cpu().numpy(), do)
     assert env.error_flags() == 0
+
+
+def test_bots_with_lookahead():
+    """k_bot of the next tick on the side stream (mrts_set_bot_lookahead(h, 1)) == oracle"""
+    lockstep(["coacAI", "workerRushAI", "randomBiasedAI", "lightRushAI"] * 3, "maps/16x16/basesWorkers16x16.xml", 2, 300,
+             max_steps=150, bot_lookahead=True)
+
+
+def test_bot_lookahead_with_map_cycling_and_resets():
+    """Look-ahead on vs off through map-cycling resets (mrts_reset_games joins the side
+    stream before it rewrites state, then re-launches) and explicit reset() calls."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+
+    cyc = ["maps/16x16/basesWorkers16x16A.xml", "maps/16x16/basesWorkers16x16B.xml", "maps/16x16/TwoBasesBarracks16x16.xml"]
+    envs = [MicroRTSGridModeVecEnv(num_selfplay_envs=2, num_bot_envs=6, max_steps=40, map_paths=[cyc[0]], cycle_maps=cyc,
+                                   ai2s=[microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.lightRushAI] * 2,
+                                   reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), return_tensors=True,
+                                   bot_lookahead=la) for la in (True, False)]
+    from oracle_py import sample_actions
+
+    for rep in range(2):
+        obs = [e.reset() for e in envs]
+        torch.testing.assert_close(obs[0], obs[1], rtol=0, atol=0)
+        for s in range(130):
+            masks = [e.get_action_mask() for e in envs]
+            assert torch.equal(masks[0], masks[1]), f"mask rep {rep} step {s}"
+            a = torch.from_numpy(sample_actions(masks[0].cpu().numpy(), 3 + rep, s)).to(envs[0].device)
+            outs = [e.step(a) for e in envs]
+            assert torch.equal(outs[0][0], outs[1][0]), f"obs rep {rep} step {s}"
+            assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+    for e in envs:
+        assert e.error_flags() == 0
+        e.close()
