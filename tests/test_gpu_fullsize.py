@@ -1,0 +1,83 @@
+"""Parity at BASELINE.json's full sizes: the product path (MicroRTSGridModeVecEnv ->
+libmicrorts_amd.so, device tensors as bench.py uses them) against the oracle
+(oracle/libmrts_oracle.so, OpenMP over games) over every env of the configuration
+the headline metric is quoted on and of configs[1] / configs[3] / 24x24.
+
+Every step compares the whole (N, HW, 78) mask, source mask, (N, H, W, P) obs, the
+raw (N, 6) rewards, the weighted reward and done, on the device.  Actions are the
+Philox masked sampler's (oracle_py.sample_actions == mrts_sample_actions, pinned by
+test_gpu_parity.py::test_device_sampler_matches_oracle_sampler).  Small `max_steps`
+put the auto-reset of every game inside the window.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MAPS
+
+pytestmark = pytest.mark.gpu
+
+W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+
+
+def _full_rollout(map_path, nsp, nbot, bot, steps, max_steps, partial_obs=False, seed=2024):
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv, sample_actions
+
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=max_steps, map_paths=[map_path],
+                               ai2s=[getattr(microrts_ai, bot)] * nbot, partial_obs=partial_obs, reward_weight=W,
+                               return_tensors=True, obs_dtype=torch.int32)
+    o = OracleVecEnv(nsp, nbot, [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=[bot] * nbot,
+                     partial_obs=partial_obs, reward_weight=W)
+    dev = g.device
+
+    def same(gpu, host, what, s):
+        assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"{what} differs at step {s}"
+
+    same(g.reset(), o.reset(), "reset obs", -1)
+    resets = 0
+    for s in range(steps):
+        mg, mo = g.get_action_mask(), o.get_action_mask()
+        same(mg, mo, "mask", s)
+        same(g.source_unit_mask, o.source_unit_mask, "source mask", s)
+        a = sample_actions(mo, seed, s)
+        og, rg, dg, ig = g.step(torch.from_numpy(a).to(dev))
+        oo, ro, do, io = o.step(a)
+        same(og, oo, "obs", s)
+        same(ig._raw, np.array([i["raw_rewards"] for i in io]), "raw rewards", s)
+        assert np.allclose(rg.cpu().numpy(), ro, rtol=0, atol=1e-12), f"weighted reward differs at step {s}"
+        same(dg, np.asarray(do, bool), "done", s)
+        resets += int(np.asarray(do).sum())
+    assert g.error_flags() == 0
+    g.close()
+    o.close()
+    return resets
+
+
+@pytest.mark.timeout(900)
+def test_fullsize_selfplay_8192_basesWorkers16x16():
+    """The headline configuration: 8192 selfplay envs (4096 games), 16x16 basesWorkers."""
+    resets = _full_rollout("maps/16x16/basesWorkers16x16.xml", 8192, 0, "passiveAI", steps=120, max_steps=100)
+    assert resets >= 8192   # every env passed through the time-limit reset
+
+
+@pytest.mark.timeout(900)
+def test_fullsize_coacai_1024():
+    """configs[1]: 1024 envs vs device coacAI."""
+    _full_rollout("maps/16x16/basesWorkers16x16.xml", 0, 1024, "coacAI", steps=500, max_steps=400)
+
+
+@pytest.mark.timeout(900)
+def test_fullsize_partial_obs_4096():
+    """configs[3]'s env: partial_obs (31 planes), 4096 envs."""
+    _full_rollout("maps/16x16/basesWorkers16x16.xml", 4096, 0, "passiveAI", steps=120, max_steps=100, partial_obs=True)
+
+
+@pytest.mark.timeout(900)
+def test_fullsize_24x24_4096():
+    """configs[4]'s largest bucket map at 4096 envs, with workerRush bot envs."""
+    _full_rollout("maps/24x24/basesWorkers24x24.xml", 2048, 2048, "workerRushAI", steps=100, max_steps=80)
