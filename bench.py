@@ -46,6 +46,9 @@ def parse():
                     help="record per-launch HIP events on every N-th step of the timed region")
     ap.add_argument("--bot-lookahead", action="store_true",
                     help="run the next tick's k_bot on a side stream right after each step (mrts_set_bot_lookahead)")
+    ap.add_argument("--api", default="tensor", choices=["tensor", "numpy"],
+                    help="numpy: the reference's host contract (numpy obs / masks / rewards out, host int64 actions in), "
+                         "i.e. the PCIe-inclusive rate; tensor: device tensors (the headline)")
     ap.add_argument("--no-eager-masks", action="store_true",
                     help="get_action_mask() launches k_masks instead of k_step writing the next tick's masks")
     ap.add_argument("--sampler", default="src", choices=["src", "dense"],
@@ -195,8 +198,9 @@ def run_gpu(args, rank, world, local_rank):
     nbot = n if nbot == "all" else nbot
     env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
                                  ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
-                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, return_tensors=True,
-                                 eager_masks=not args.no_eager_masks, bot_lookahead=args.bot_lookahead)
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev,
+                                 return_tensors=args.api == "tensor", eager_masks=not args.no_eager_masks,
+                                 bot_lookahead=args.bot_lookahead)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
     lib = _native.lib()
@@ -209,15 +213,17 @@ def run_gpu(args, rank, world, local_rank):
         # timed region (each event is a queue packet between dependent kernels;
         # recording all of them costs ~7 % of the step)
         env.kernel_events = ev if (timing[0] and s % args.event_every == 0) else None
-        m = env.get_action_mask()
+        m = env.get_action_mask()   # numpy api: the (N, HW, 78) host copy ppo_gridnet.py:466 makes
         if env.kernel_events is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        rc = sample(lib, args.sampler, m, env.source_unit_mask, n, hw, seed, s, act)
+        rc = sample(lib, args.sampler, env._mask, env._src, n, hw, seed, s, act)
         if env.kernel_events is not None:
             e1.record()
             env.kernel_events.setdefault("sample", []).append((e0, e1))
         _native.check(rc, None, "sample")
+        if args.api == "numpy":   # ppo_gridnet.py:475: host int64 actions (N, HW*7)
+            return env.step(act.cpu().numpy().reshape(n, -1))
         return env.step(act)
 
     timing = [False]
@@ -238,7 +244,7 @@ def run_gpu(args, rank, world, local_rank):
     flags = env.error_flags()
     kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
     G = nsp // 2 + nbot
-    src_rows = int(env.source_unit_mask.sum().item())   # source cells of the last step (sampler bytes)
+    src_rows = int(env._src.sum().item())   # source cells of the last step (sampler bytes)
     return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes), src_rows
 
 
@@ -378,6 +384,9 @@ def main():
         }
         if args.workload != "selfplay":
             out["metric"] = f"env-steps/sec, workload {args.workload} (secondary config, not the BASELINE metric)"
+        if args.api == "numpy":
+            out["metric"] = ("env-steps/sec, reference numpy contract (obs / masks / rewards copied to the host, host "
+                             "actions in: PCIe-inclusive; not the headline)")
         if world == 1 and not args.no_cpu_baseline and args.workload == "selfplay":
             out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
