@@ -46,9 +46,10 @@ def parse():
                     help="record per-launch HIP events on every N-th step of the timed region")
     ap.add_argument("--bot-lookahead", action="store_true",
                     help="run the next tick's k_bot on a side stream right after each step (mrts_set_bot_lookahead)")
-    ap.add_argument("--api", default="tensor", choices=["tensor", "numpy"],
+    ap.add_argument("--api", default="tensor", choices=["tensor", "numpy", "sharedmem"],
                     help="numpy: the reference's host contract (numpy obs / masks / rewards out, host int64 actions in), "
-                         "i.e. the PCIe-inclusive rate; tensor: device tensors (the headline)")
+                         "i.e. the PCIe-inclusive rate; sharedmem: the same through MicroRTSGridModeSharedMemVecEnv's "
+                         "page-locked buffers; tensor: device tensors (the headline)")
     ap.add_argument("--no-eager-masks", action="store_true",
                     help="get_action_mask() launches k_masks instead of k_step writing the next tick's masks")
     ap.add_argument("--sampler", default="src", choices=["src", "dense"],
@@ -196,11 +197,16 @@ def run_gpu(args, rank, world, local_rank):
     wmap, nsp, nbot, bot, po = WORKLOADS[args.workload]
     nsp = n if nsp == "all" else nsp
     nbot = n if nbot == "all" else nbot
-    env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
-                                 ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
-                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev,
-                                 return_tensors=args.api == "tensor", eager_masks=not args.no_eager_masks,
-                                 bot_lookahead=args.bot_lookahead)
+    if args.api == "sharedmem":
+        from gym_microrts.envs.vec_env import MicroRTSGridModeSharedMemVecEnv as Env
+        extra = {}
+    else:
+        Env = MicroRTSGridModeVecEnv
+        extra = dict(return_tensors=args.api == "tensor", eager_masks=not args.no_eager_masks,
+                     bot_lookahead=args.bot_lookahead)
+    env = Env(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
+              ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
+              reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, **extra)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
     lib = _native.lib()
@@ -222,7 +228,7 @@ def run_gpu(args, rank, world, local_rank):
             e1.record()
             env.kernel_events.setdefault("sample", []).append((e0, e1))
         _native.check(rc, None, "sample")
-        if args.api == "numpy":   # ppo_gridnet.py:475: host int64 actions (N, HW*7)
+        if args.api != "tensor":   # ppo_gridnet.py:475: host int64 actions (N, HW*7)
             return env.step(act.cpu().numpy().reshape(n, -1))
         return env.step(act)
 
@@ -384,7 +390,8 @@ def main():
         }
         if args.workload != "selfplay":
             out["metric"] = f"env-steps/sec, workload {args.workload} (secondary config, not the BASELINE metric)"
-        if args.api == "numpy":
+        if args.api != "tensor":
+            out["config"]["api"] = args.api
             out["metric"] = ("env-steps/sec, reference numpy contract (obs / masks / rewards copied to the host, host "
                              "actions in: PCIe-inclusive; not the headline)")
         if world == 1 and not args.no_cpu_baseline and args.workload == "selfplay":

@@ -472,6 +472,77 @@ class MicroRTSBotVecEnv(MicroRTSGridModeVecEnv):
         return np.ones((self.num_envs, 2)), reward @ self.reward_weight, done[:, 0], infos
 
 
+class MicroRTSGridModeSharedMemVecEnv(MicroRTSGridModeVecEnv):
+    """vec_env.py:1238-1362: the zero-copy variant.  The reference allocates three
+    direct buffers shared with the JVM (`self.obs` (N, H, W, P) int32,
+    `self.action_mask` (N, H*W, 78) int32, `self.actions` (N, H*W, 7) int32) and
+    returns them from reset / step / get_action_mask, overwritten in place by every
+    call; all envs play one map.
+
+    Here the three are page-locked host arrays: the engine's device outputs are
+    copied into them (one DMA each, no allocation) and `self.actions` is copied to
+    the device by `step_wait`, with the same aliasing contract.  Rewards are
+    `raw @ reward_weight` in numpy, dones `done[:, 0]`, infos `[{"raw_rewards": r}]`.
+    The reference forwards its arguments to the base class by position, which
+    shifts `reward_weight` into `reward_shaping`; they are
+    forwarded by name here."""
+
+    def __init__(
+        self,
+        num_selfplay_envs,
+        num_bot_envs,
+        partial_obs=False,
+        max_steps=2000,
+        render_theme=2,
+        frame_skip=0,
+        ai2s=[],
+        map_paths=["maps/10x10/basesTwoWorkers10x10.xml"],
+        reward_weight=np.array([0.0, 1.0, 0.0, 0.0, 0.0, 5.0]),
+        cycle_maps=[],
+        *,
+        device=None,
+    ):
+        if len(map_paths) > 1 and len(set(map_paths)) > 1:
+            raise ValueError("Mem shared environment requires all games to be played on the same map.")
+        super().__init__(num_selfplay_envs, num_bot_envs, partial_obs=partial_obs, max_steps=max_steps,
+                         render_theme=render_theme, frame_skip=frame_skip, ai2s=ai2s, map_paths=map_paths,
+                         reward_weight=reward_weight, cycle_maps=cycle_maps, device=device, return_tensors=True,
+                         obs_dtype=torch.int32)
+        hw = self.height * self.width
+        self.num_feature_planes = self._obs.shape[-1]
+        self.masks_dim = sum(self.action_space_dims)
+        self.action_dim = len(self.action_space_dims)
+        pin = self.device.type == "cuda"
+        self._obs_host = torch.empty(tuple(self._obs.shape), dtype=torch.int32, pin_memory=pin)
+        self._mask_host = torch.empty((self.num_envs, hw, self.masks_dim), dtype=torch.int32, pin_memory=pin)
+        self._act_host = torch.zeros((self.num_envs, hw, self.action_dim), dtype=torch.int32, pin_memory=pin)
+        self._act_dev32 = torch.empty((self.num_envs, hw, self.action_dim), dtype=torch.int32, device=self.device)
+        self.obs = self._obs_host.numpy()
+        self.action_mask = self._mask_host.numpy()
+        self.actions = self._act_host.numpy()
+
+    def reset(self):
+        self._obs_host.copy_(super().reset())
+        return self.obs
+
+    def get_action_mask(self):
+        self._mask_host.copy_(super().get_action_mask())
+        return self.action_mask
+
+    def step_async(self, actions):
+        actions = np.asarray(actions).reshape((self.num_envs, self.width * self.height, self.action_dim))
+        np.copyto(self.actions, actions)
+        # int32 over PCIe from the page-locked buffer, widened to int64 on the device
+        self._act_dev32.copy_(self._act_host, non_blocking=True)
+        super().step_async(self._act_dev32)
+
+    def step_wait(self):
+        obs, _, done0, infos = super().step_wait()
+        self._obs_host.copy_(obs)
+        reward = infos._raw.cpu().numpy()
+        return self.obs, reward @ self.reward_weight, done0.cpu().numpy(), [{"raw_rewards": r} for r in reward]
+
+
 class MicroRTSMixedMapVecEnv:
     """Maps of several sizes in one batch (BASELINE.json config 5), bucketed by
     height x width: one MicroRTSGridModeVecEnv engine per bucket, all launched on
