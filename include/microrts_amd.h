@@ -106,18 +106,17 @@ int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source);
  * before it rewrites them).  NULL, NULL unbinds. */
 int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source);
 
-/* Bot look-ahead (default off).  A bot's getAction(1, gs) reads only the state
- * before the tick (JNIGridnetClient.gameStep: bot decision, then issueSafe(p0),
- * issueSafe(p1), cycle), so once mrts_step / mrts_reset / mrts_reset_games has
- * left a state, the next tick's bot decisions (k_bot) are launched on an
- * engine-owned side stream, ordered after that state by an event, and overlap
- * whatever the caller runs before the next mrts_step (its policy network).  The
- * next mrts_step / reset / error-flags read waits on them with an event; outputs
- * are identical either way.  on = 0 (default) runs k_bot inline at the start of
- * each step: measured on MI355X, the cross-stream event handoff costs more than
- * the overlap gains when the caller's work between steps is short (bench: coacAI
- * 1024 envs 13.1 M inline vs 10.9 M look-ahead env-steps/s). */
-int mrts_set_bot_lookahead(mrts_vec *h, int32_t on);
+/* Bot fusion (default on).  A bot's getAction(1, gs) reads only the state
+ * before the tick (JNIGridnetClient.gameStep: bot decisions, then issueSafe(p0),
+ * issueSafe(p1), cycle).  With fusion, mrts_step's kernel decides the NEXT
+ * tick's bot actions for every bot game in the same pass -- one wavefront of the
+ * game's workgroup runs the bot on the state it has just stored while the other
+ * wavefronts stream the observations and masks -- instead of a separate bot
+ * kernel at the start of the next step; mrts_reset / mrts_reset_games decide
+ * them for the games they reset.  Outputs are identical either way.  Applies
+ * when no env has a bot as player 0 (MicroRTSBotVecEnv) and the map's two LDS
+ * regions fit one workgroup; on = 0 launches the bot kernel at every step. */
+int mrts_set_bot_fusion(mrts_vec *h, int32_t on);
 
 /* step_async + JNIGridnetVecClient.gameStep (vec_env.py:968-984, 1002):
  * actions [N][H*W][7] int64 (device), source [N][H*W] int32 = the source

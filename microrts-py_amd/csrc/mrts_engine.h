@@ -32,6 +32,9 @@ struct EngineParams {
     int4 *aa;               // [Gb][2][HW][2] AbstractionLayerAI.actions per bot player
     int32_t *botpa;         // [Gb][2][HW] bot PlayerActions, cell | code << 16; null = none
     int nbot_active;        // bot players (either side) whose AI is not passiveAI
+    const int32_t *bot_games; // k_bot: decide only for these games (device list), null = every bot game
+    int bot_ngames;
+    int fuse_bots;          // k_step: wave 0 of each bot game's workgroup decides the next tick's bot actions
 };
 
 extern "C" {
@@ -46,5 +49,6 @@ hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n
 hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, int map, int size, uint8_t *rgb);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);
+int mrts_engine_fused_capacity(const EngineParams *p);
 }
 #endif

@@ -28,6 +28,7 @@
 #include "mrts_layout.h"
 
 #include "mrts_rules.h"
+#include "mrts_bots.h"
 
 namespace mrts {
 
@@ -237,8 +238,11 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
 // further barrier (the envs of a game are adjacent: a selfplay pair 2k, 2k+1
 // writes one contiguous run).  The words live in the region of the step's
 // scratch lists (resv .. snap), dead by now.
+// `skip`: lanes [0, skip) leave after phase A (the bot-fused k_step's wave 0) and
+// the others stream phase B alone.
 template <int NT, int P, typename OT>
-__device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks) {
+__device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks,
+                                             int skip = 0) {
     const int HW = p.HW, NV = G.nviews;
     uint32_t* ow = L.outw;            // [NV][HW]    one-hot bits
     uint32_t* mw = L.outw + 2 * HW;   // [NV][HW][3] mask bits (bit 0 = source)
@@ -269,12 +273,14 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
         }
     }
     __syncthreads();
+    if ((int)threadIdx.x < skip) return;
+    const int t0 = (int)threadIdx.x - skip, nt = NT - skip;
     if (obs) {
         OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P;
         const int total = NV * HW * P;
         if (((HW * P) & 3) == 0) {   // every env's rows start 16-B aligned
             constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
-            for (int k = threadIdx.x; k < total / 4; k += NT) {
+            for (int k = t0; k < total / 4; k += nt) {
                 const int e = 4 * k;
                 int c = e / P, pl = e - c * P;
                 int v[4];
@@ -286,14 +292,14 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
                 st16(out + e, v[0], v[1], v[2], v[3]);
             }
         } else {
-            for (int e = threadIdx.x; e < total; e += NT) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
+            for (int e = t0; e < total; e += nt) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
         }
     }
     if (masks) {
         int32_t* out = p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH;
         const int total = NV * HW * MRTS_MASK_CH;
         if ((HW & 1) == 0) {   // HW * 78 % 4 == 0: every env's rows start 16-B aligned
-            for (int k = threadIdx.x; k < total / 4; k += NT) {
+            for (int k = t0; k < total / 4; k += nt) {
                 const int e = 4 * k;
                 int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
                 int v4[4];
@@ -306,7 +312,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
                 st16(out + e, v4[0], v4[1], v4[2], v4[3]);
             }
         } else {
-            for (int e = threadIdx.x; e < total; e += NT) {
+            for (int e = t0; e < total; e += nt) {
                 const int r = e / MRTS_MASK_CH, b = e % MRTS_MASK_CH + 1;
                 out[e] = (int)((mw[3 * r + (b >> 5)] >> (b & 31)) & 1u);
             }
@@ -647,7 +653,10 @@ __device__ __forceinline__ int step_game_index(int G) {
 // b + gridDim.x, ..., prefetching the next game's state during the current
 // game's output stream (measured: hipcc's allocation of the looped body takes
 // 164 VGPRs, occupancy 3 -- DESIGN.md §5).
-template <int NT, int P, typename OT>
+// FB (bot fusion, p.fuse_bots): in a bot game's workgroup, wave 0 decides the
+// NEXT tick's bot actions (bots::bot_game on the state just stored) while waves
+// 1.. stream this tick's outputs; its LDS follows the step's (launch_all).
+template <int NT, int P, typename OT, bool FB = false>
 __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
@@ -973,7 +982,10 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
 #else
     constexpr bool kMasks = true;
 #endif
-    emit_outputs<NT, P, OT>(p, L, G, kObs, kMasks && p.mask != nullptr);
+    const bool botg = FB && g >= p.nsp_games && NT > 64;
+    emit_outputs<NT, P, OT>(p, L, G, kObs, kMasks && p.mask != nullptr, botg ? 64 : 0);
+    if (FB && botg && threadIdx.x < 64)   // every read of the stored state is behind phase A's barrier
+        bots::bot_game<true>(p, g - p.nsp_games, 1, smem + bots::b16(lds_bytes(HW, p.W, NT)));
     __syncthreads();   // LDS is reused by the next game
     }
 }
@@ -1261,7 +1273,6 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
 // ---------------------------------------------------------------------------
 // launchers
 
-#ifdef MRTS_STEP_PERSISTENT
 // Resident capacity of a kernel on the current device (blocks per CU x CUs),
 // cached per (kernel, LDS bytes, device).
 static int resident_blocks(const void* kernel, int NT, size_t sh) {
@@ -1280,7 +1291,6 @@ static int resident_blocks(const void* kernel, int NT, size_t sh) {
     cache.push_back({kernel, sh, dev, cus * per});
     return cus * per;
 }
-#endif
 
 template <typename K>
 static void launch_step(K kernel, int NT, size_t sh, hipStream_t s, const EngineParams& p) {
@@ -1311,6 +1321,15 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
         }
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
+    } else if (p.fuse_bots && NT > 64) {
+        sh = bots::b16(sh) + bots::bot_lds_bytes(p.HW, p.W);
+        if (p.partial_obs) {
+            if (p.obs_float) launch_step(k_step<NT, 31, float, true>, NT, sh, s, p);
+            else launch_step(k_step<NT, 31, int32_t, true>, NT, sh, s, p);
+        } else {
+            if (p.obs_float) launch_step(k_step<NT, 29, float, true>, NT, sh, s, p);
+            else launch_step(k_step<NT, 29, int32_t, true>, NT, sh, s, p);
+        }
     } else {
         if (p.partial_obs) {
             if (p.obs_float) launch_step(k_step<NT, 31, float>, NT, sh, s, p);
@@ -1370,6 +1389,24 @@ hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, in
     hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->HW, p->map_wall + (size_t)map * p->HW,
                        p->W, p->H, size, rgb);
     return hipGetLastError();
+}
+// Resident workgroups of the bot-fused k_step for this map on the current device
+// (0: no fused variant).  The host fuses only when every game's workgroup is
+// resident at once: with more games, the fused variant's occupancy (86 VGPRs,
+// step + bot LDS) costs more than the separate k_bot launch it saves.
+int mrts_engine_fused_capacity(const EngineParams* p) {
+    using namespace mrts;
+    if (p->HW <= 64) return 0;
+    const int NT = p->HW <= 128 ? 128 : 256;
+    const size_t sh = bots::b16(lds_bytes(p->HW, p->W, NT)) + bots::bot_lds_bytes(p->HW, p->W);
+    const void* k;
+    if (NT == 128)
+        k = p->partial_obs ? (p->obs_float ? (const void*)k_step<128, 31, float, true> : (const void*)k_step<128, 31, int32_t, true>)
+                           : (p->obs_float ? (const void*)k_step<128, 29, float, true> : (const void*)k_step<128, 29, int32_t, true>);
+    else
+        k = p->partial_obs ? (p->obs_float ? (const void*)k_step<256, 31, float, true> : (const void*)k_step<256, 31, int32_t, true>)
+                           : (p->obs_float ? (const void*)k_step<256, 29, float, true> : (const void*)k_step<256, 29, int32_t, true>);
+    return resident_blocks(k, NT, sh);
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {
     int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;

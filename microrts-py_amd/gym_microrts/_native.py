@@ -77,7 +77,7 @@ SIGNATURES = {
     "mrts_sample_actions": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
     "mrts_sample_actions_src": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
     "mrts_bind_mask_outputs": (ctypes.c_int, [P, P, P]),
-    "mrts_set_bot_lookahead": (ctypes.c_int, [P, ctypes.c_int32]),
+    "mrts_set_bot_fusion": (ctypes.c_int, [P, ctypes.c_int32]),
     "mrts_render": (ctypes.c_int, [P, P, ctypes.c_int32, P, ctypes.c_int32]),
     "mrts_error_flags": (ctypes.c_int, [P, P, P]),
     "mrts_utt_json": (ctypes.c_char_p, [P]),

@@ -127,7 +127,7 @@ class MicroRTSGridModeVecEnv:
         return_tensors=False,
         obs_dtype=None,
         eager_masks=True,
-        bot_lookahead=False,
+        bot_fusion=True,
         _ai1s=None,
     ):
         # vec_env.py:110-127
@@ -237,12 +237,10 @@ class MicroRTSGridModeVecEnv:
         if self.eager_masks:
             _native.check(_native.lib().mrts_bind_mask_outputs(self._h, self._mask.data_ptr(), self._src.data_ptr()), self._h,
                           "bind_mask_outputs")
-        # bot look-ahead (opt-in): the device bots' decisions for the next tick run on
-        # a side stream right after reset / step, overlapping the caller's policy
-        # (mrts_set_bot_lookahead; outputs identical either way; off by default:
-        # the cross-stream handoff costs more than it hides in short loops)
-        self.bot_lookahead = bool(bot_lookahead)
-        _native.check(_native.lib().mrts_set_bot_lookahead(self._h, int(self.bot_lookahead)), self._h, "set_bot_lookahead")
+        # bot fusion: the step kernel decides the next tick's device-bot actions in
+        # the same pass (mrts_set_bot_fusion; outputs identical either way)
+        self.bot_fusion = bool(bot_fusion)
+        _native.check(_native.lib().mrts_set_bot_fusion(self._h, int(self.bot_fusion)), self._h, "set_bot_fusion")
 
         # computed properties (vec_env.py:230-254)
         self.action_space_dims = [6, 4, 4, 4, 4, len(self.utt["unitTypes"]), 7 * 7]

@@ -16,7 +16,7 @@ BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "POWorkerRush
 
 
 def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=2000, mode="masked", return_tensors=False,
-             bot_lookahead=False):
+             bot_fusion=True):
     import torch
 
     from gym_microrts import microrts_ai
@@ -27,7 +27,7 @@ def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=200
     g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=len(ais), max_steps=max_steps,
                                ai2s=[getattr(microrts_ai, a) for a in ais], map_paths=[map_path], reward_weight=w,
                                partial_obs=partial_obs, return_tensors=return_tensors,
-                               obs_dtype=torch.int32 if return_tensors else None, bot_lookahead=bot_lookahead)
+                               obs_dtype=torch.int32 if return_tensors else None, bot_fusion=bot_fusion)
     o = OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais,
                      partial_obs=partial_obs, reward_weight=w)
     cpu = (lambda t: t.cpu().numpy()) if return_tensors else np.asarray
@@ -153,15 +153,15 @@ def test_mixed_map_buckets_match_oracle():
     assert env.error_flags() == 0
 
 
-def test_bots_with_lookahead():
-    """k_bot of the next tick on the side stream (mrts_set_bot_lookahead(h, 1)) == oracle"""
+def test_bots_without_fusion():
+    """k_bot launched at the start of every step (mrts_set_bot_fusion(h, 0)) == oracle"""
     lockstep(["coacAI", "workerRushAI", "randomBiasedAI", "lightRushAI"] * 3, "maps/16x16/basesWorkers16x16.xml", 2, 300,
-             max_steps=150, bot_lookahead=True)
+             max_steps=150, bot_fusion=False)
 
 
-def test_bot_lookahead_with_map_cycling_and_resets():
-    """Look-ahead on vs off through map-cycling resets (mrts_reset_games joins the side
-    stream before it rewrites state, then re-launches) and explicit reset() calls."""
+def test_bot_fusion_with_map_cycling_and_resets():
+    """Fusion on vs off through map-cycling resets (mrts_reset_games decides the reset
+    games' bot actions afresh) and explicit reset() calls."""
     import torch
 
     from gym_microrts import microrts_ai
@@ -171,7 +171,7 @@ def test_bot_lookahead_with_map_cycling_and_resets():
     envs = [MicroRTSGridModeVecEnv(num_selfplay_envs=2, num_bot_envs=6, max_steps=40, map_paths=[cyc[0]], cycle_maps=cyc,
                                    ai2s=[microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.lightRushAI] * 2,
                                    reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), return_tensors=True,
-                                   bot_lookahead=la) for la in (True, False)]
+                                   bot_fusion=fu) for fu in (True, False)]
     from oracle_py import sample_actions
 
     for rep in range(2):
