@@ -44,8 +44,8 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true")
     ap.add_argument("--event-every", type=int, default=8,
                     help="record per-launch HIP events on every N-th step of the timed region")
-    ap.add_argument("--no-bot-fusion", action="store_true",
-                    help="launch k_bot at every step instead of k_step deciding the next tick's bot actions")
+    ap.add_argument("--bot-fusion", type=int, default=1, choices=[0, 1],
+                    help="mrts_set_bot_fusion: 0 k_bot at every step, 1 k_step decides the next tick's bot actions")
     ap.add_argument("--api", default="tensor", choices=["tensor", "numpy", "sharedmem"],
                     help="numpy: the reference's host contract (numpy obs / masks / rewards out, host int64 actions in), "
                          "i.e. the PCIe-inclusive rate; sharedmem: the same through MicroRTSGridModeSharedMemVecEnv's "
@@ -203,7 +203,7 @@ def run_gpu(args, rank, world, local_rank):
     else:
         Env = MicroRTSGridModeVecEnv
         extra = dict(return_tensors=args.api == "tensor", eager_masks=not args.no_eager_masks,
-                     bot_fusion=not args.no_bot_fusion)
+                     bot_fusion=args.bot_fusion)
     env = Env(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
               ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
               reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, **extra)

@@ -77,7 +77,7 @@ __host__ __device__ inline size_t bot_lds_bytes(int HW, int W) {
            b16((size_t)HW) + b16(4 * 32);
 }
 
-__device__ inline BL bot_carve(unsigned char* base, int HW, int W) {
+__device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W) {
     BL L;
     size_t o = 0;
     auto take = [&](size_t n) { unsigned char* p = base + o; o += b16(n); return p; };
@@ -122,7 +122,7 @@ __device__ __forceinline__ bool v_free(const BS& S, const BL& L, int x, int y) {
 }
 
 // uid -> cell in the bot's view (binary search over the uid-ordered list), -1 if absent
-__device__ int cell_of_uid(const BS& S, const BL& L, int uid) {
+__device__ __forceinline__ int cell_of_uid(const BS& S, const BL& L, int uid) {
     int lo = 0, hi = S.n - 1;
     while (lo <= hi) {
         int mid = (lo + hi) >> 1, v = L.uuid[mid];
@@ -194,9 +194,12 @@ __device__ __forceinline__ RU usage(const BS& S, int c, int code, int owner) {  
     RU r{-0x7fffffff, {0, 0}};
     const int t = code_type(code);
     if (t == A_MOVE || t == A_PRODUCE) {
-        const int off[4] = {-S.W, 1, S.W, -1};
-        r.pos = c + off[code_param(code)];
-        if (t == A_PRODUCE) r.res[owner] = ut_cost(code_utype(code));
+        const int d = code_param(code);   // selects, not an indexed local array (scratch)
+        r.pos = c + (d == 0 ? -S.W : d == 1 ? 1 : d == 2 ? S.W : -1);
+        if (t == A_PRODUCE) {
+            if (owner == 0) r.res[0] = ut_cost(code_utype(code));
+            else if (owner == 1) r.res[1] = ut_cost(code_utype(code));
+        }
     }
     return r;
 }
@@ -212,7 +215,7 @@ __device__ __forceinline__ bool consistent(const BS& S, const RU& r, const uint3
 }
 
 // GameState.isUnitActionAllowed on the bot's state
-__device__ bool allowed(const BS& S, const BL& L, int c, int code) {
+__device__ __forceinline__ bool allowed(const BS& S, const BL& L, int c, int code) {
     if (code_type(code) == A_MOVE) {
         int n = nb_cell(Grid{S.W, S.H, S.HW}, c, code_param(code));
         if (n < 0 || L.wall[n] || L.unit[n] != 0) return false;
@@ -222,7 +225,7 @@ __device__ bool allowed(const BS& S, const BL& L, int c, int code) {
 }
 
 // PlayerAction.addUnitAction + ResourceUsage.merge
-__device__ void pa_add(BS& S, const BL& L, int c, int code) {
+__device__ __forceinline__ void pa_add(BS& S, const BL& L, int c, int code) {
     RU r = usage(S, c, code, u_owner(L.unit[c]));
     if (lane0()) {
         L.pa[S.npa] = c | (code << 16);
@@ -242,7 +245,7 @@ __device__ void pa_add(BS& S, const BL& L, int c, int code) {
 // Breadth-first layers grow from the goal set (free cells within `range` of
 // the target) over free cells; the first layer that touches a free neighbour
 // of the start decides the move, ties UP, RIGHT, DOWN, LEFT.  -1 = null.
-__device__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
+__device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
 #ifdef MRTS_EXP_NOPF   // kernel-variant experiments only: path finding skipped (behaviour changes)
     return -1;
 #endif
@@ -280,7 +283,7 @@ __device__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
 }
 
 // ---- abstract actions ----------------------------------------------------------
-__device__ int find_aa(const BS& S, const BL& L, int uid) {   // first entry of the unit, lane-parallel
+__device__ __forceinline__ int find_aa(const BS& S, const BL& L, int uid) {   // first entry of the unit, lane-parallel
     for (int base = 0; base < S.naa; base += BT) {
         const int k = base + threadIdx.x;
         const unsigned long long m = __ballot(k < S.naa && L.aa[2 * k].x == uid);
@@ -288,7 +291,7 @@ __device__ int find_aa(const BS& S, const BL& L, int uid) {   // first entry of 
     }
     return -1;
 }
-__device__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   // actions.put(u, aa)
+__device__ __forceinline__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   // actions.put(u, aa)
     int k = find_aa(S, L, a.x);
     if (k < 0) {
         if (S.naa >= S.HW) {   // more live entries than cells: cannot happen on legal states
@@ -302,23 +305,23 @@ __device__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   // actions.put(u,
         L.aa[2 * k + 1] = b;
     }
 }
-__device__ void ab_move(BS& S, const BL& L, int uid, int x, int y) {
+__device__ __forceinline__ void ab_move(BS& S, const BL& L, int uid, int x, int y) {
     aa_put(S, L, make_int4(uid, AA_MOVE, -1, pk_xy(x, y)), make_int4(-1, 0, 0, 0));
 }
-__device__ void ab_train(BS& S, const BL& L, int uid, int t) {
+__device__ __forceinline__ void ab_train(BS& S, const BL& L, int uid, int t) {
     aa_put(S, L, make_int4(uid, AA_TRAIN | (t << 4), -1, 0), make_int4(-1, 0, 0, 0));
 }
-__device__ void ab_build(BS& S, const BL& L, int uid, int t, int x, int y) {
+__device__ __forceinline__ void ab_build(BS& S, const BL& L, int uid, int t, int x, int y) {
     aa_put(S, L, make_int4(uid, AA_BUILD | (t << 4), -1, pk_xy(x, y)), make_int4(-1, 0, 0, 0));
 }
-__device__ void ab_harvest(BS& S, const BL& L, int uid, int res_uid, int base_uid, int base_cell) {
+__device__ __forceinline__ void ab_harvest(BS& S, const BL& L, int uid, int res_uid, int base_uid, int base_cell) {
     aa_put(S, L, make_int4(uid, AA_HARVEST, res_uid, 0), make_int4(base_uid, pk_xy(base_cell % S.W, base_cell / S.W), 0, 0));
 }
-__device__ void ab_attack(BS& S, const BL& L, int uid, int target_uid) {
+__device__ __forceinline__ void ab_attack(BS& S, const BL& L, int uid, int target_uid) {
     aa_put(S, L, make_int4(uid, AA_ATTACK, target_uid, 0), make_int4(-1, 0, 0, 0));
 }
 
-__device__ int adj_dir(int ux, int uy, int x, int y) {
+__device__ __forceinline__ int adj_dir(int ux, int uy, int x, int y) {
     if (x == ux && y == uy - 1) return 0;
     if (x == ux + 1 && y == uy) return 1;
     if (x == ux && y == uy + 1) return 2;
@@ -326,7 +329,7 @@ __device__ int adj_dir(int ux, int uy, int x, int y) {
     return -1;
 }
 
-__device__ int train_score(const BS& S, const BL& L, int x, int y, int type, int player) {   // Train.score
+__device__ __forceinline__ int train_score(const BS& S, const BL& L, int x, int y, int type, int player) {   // Train.score
     int dist = 0;   // stays 0 when nothing qualifies
     closest_unit(S, L, x, y, [&](int c) {
         const uint32_t o = L.unit[c];
@@ -335,7 +338,7 @@ __device__ int train_score(const BS& S, const BL& L, int x, int y, int type, int
     return -dist;
 }
 
-__device__ bool aa_completed(const BS& S, const BL& L, int4 a, int cu) {
+__device__ __forceinline__ bool aa_completed(const BS& S, const BL& L, int4 a, int cu) {
     switch (aa_kind(a)) {
     case AA_MOVE: return cu % S.W == pk_x(a.w) && cu / S.W == pk_y(a.w);
     case AA_HARVEST:
@@ -345,7 +348,7 @@ __device__ bool aa_completed(const BS& S, const BL& L, int4 a, int cu) {
 }
 
 // AbstractAction.execute: action code, or -1 for null; may set `completed`
-__device__ int aa_execute(const BS& S, const BL& L, int4& a, int4 b, int cu) {
+__device__ __forceinline__ int aa_execute(const BS& S, const BL& L, int4& a, int4 b, int cu) {
     const uint32_t u = L.unit[cu];
     const int ux = cu % S.W, uy = cu / S.W;
     switch (aa_kind(a)) {
@@ -420,7 +423,7 @@ __device__ int aa_execute(const BS& S, const BL& L, int4& a, int4 b, int cu) {
 }
 
 // AbstractionLayerAI.translateActions (fillWithNones(gs, p, 1) is k_step's phase 3)
-__device__ void translate_actions(BS& S, const BL& L) {
+__device__ __forceinline__ void translate_actions(BS& S, const BL& L) {
     int w = 0;
     const int n0 = S.naa;
     for (int k = 0; k < n0; k++) {
@@ -449,7 +452,7 @@ __device__ void translate_actions(BS& S, const BL& L) {
 // ---- behaviours ------------------------------------------------------------------
 // closest enemy of the unit at cu: precomputed for every unit in k_bot before
 // the behaviours (L.pa[cell]) for the rush family; wave-parallel scan otherwise
-__device__ int closest_enemy(const BS& S, const BL& L, int cu, bool table = true) {
+__device__ __forceinline__ int closest_enemy(const BS& S, const BL& L, int cu, bool table = true) {
     if (table) return L.pa[cu];
     const int me = u_owner(L.unit[cu]);
     return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
@@ -457,7 +460,7 @@ __device__ int closest_enemy(const BS& S, const BL& L, int cu, bool table = true
         return o >= 0 && o != me;
     });
 }
-__device__ int closest_of(const BS& S, const BL& L, int cu, bool want_resource) {
+__device__ __forceinline__ int closest_of(const BS& S, const BL& L, int cu, bool want_resource) {
     const int me = u_owner(L.unit[cu]);
     return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
         const uint32_t o = L.unit[c];
@@ -466,7 +469,7 @@ __device__ int closest_of(const BS& S, const BL& L, int cu, bool want_resource) 
 }
 
 // meleeUnitBehavior (+ PO* exploration: nearest cell the player cannot observe)
-__device__ void melee_behavior(BS& S, const BL& L, int cu, bool po) {
+__device__ __forceinline__ void melee_behavior(BS& S, const BL& L, int cu, bool po) {
     const int e = closest_enemy(S, L, cu);
     if (e >= 0) {
         ab_attack(S, L, L.uid[cu], L.uid[e]);
@@ -492,7 +495,7 @@ __device__ void melee_behavior(BS& S, const BL& L, int cu, bool po) {
     }
 }
 
-__device__ void harvest_behavior(BS& S, const BL& L, int cu) {
+__device__ __forceinline__ void harvest_behavior(BS& S, const BL& L, int cu) {
     const int r = closest_of(S, L, cu, true), b = closest_of(S, L, cu, false);
     if (r < 0 || b < 0) return;
     const int k = find_aa(S, L, L.uid[cu]);
@@ -504,7 +507,11 @@ __device__ void harvest_behavior(BS& S, const BL& L, int cu) {
 }
 
 // AbstractionLayerAI.findBuildingPosition
-__device__ int find_building_position(const BS& S, const BL& L, const int* reserved, int nres, int dx, int dy) {
+// building positions reserved by this getAction (a base and a barracks at most), in registers
+struct Rsv {
+    int a, b, n;
+};
+__device__ __forceinline__ int find_building_position(const BS& S, const BL& L, const Rsv& rs, int dx, int dy) {
     const int Lmax = max(S.W, S.H);
     for (int l = 1; l < Lmax; l++) {
         for (int side = 0; side < 4; side++) {
@@ -516,8 +523,7 @@ __device__ int find_building_position(const BS& S, const BL& L, const int* reser
                 else { x = dx - l; y = dy + k; if (x < 0) break; }
                 if (!in_map(S, x, y)) continue;
                 const int pos = x + y * S.W;
-                bool taken = false;
-                for (int i = 0; i < nres; i++) taken |= reserved[i] == pos;
+                const bool taken = (rs.n > 0 && rs.a == pos) || (rs.n > 1 && rs.b == pos);
                 if (!taken && v_free(S, L, x, y)) return pos;
             }
         }
@@ -525,18 +531,20 @@ __device__ int find_building_position(const BS& S, const BL& L, const int* reser
     return -1;
 }
 
-__device__ void build_if_not_already(BS& S, const BL& L, int cu, int type, int* reserved, int& nres) {
+__device__ __forceinline__ void build_if_not_already(BS& S, const BL& L, int cu, int type, Rsv& rs) {
     const int k = find_aa(S, L, L.uid[cu]);
     if (k >= 0) {
         const int4 a = L.aa[2 * k];
         if (aa_kind(a) == AA_BUILD && aa_utype(a) == type) return;
     }
-    const int pos = find_building_position(S, L, reserved, nres, cu % S.W, cu / S.W);
+    const int pos = find_building_position(S, L, rs, cu % S.W, cu / S.W);
     ab_build(S, L, L.uid[cu], type, pos % S.W, pos / S.W);   // C/Java division: -1 -> (-1, 0)
-    reserved[nres++] = pos;
+    if (rs.n == 0) rs.a = pos;
+    else rs.b = pos;
+    rs.n++;
 }
 
-__device__ int count_units(const BS& S, const BL& L, int type, bool own) {
+__device__ __forceinline__ int count_units(const BS& S, const BL& L, int type, bool own) {
     return count_where(S, L, [&](int c) {
         const uint32_t o = L.unit[c];
         return u_type(o) == type && (own ? u_owner(o) == S.player : (u_owner(o) >= 0 && u_owner(o) != S.player));
@@ -544,8 +552,8 @@ __device__ int count_units(const BS& S, const BL& L, int type, bool own) {
 }
 
 // WorkerRush / LightRush / HeavyRush / RangedRush (+ PO*), and coacAI
-__device__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac) {
-    const int p = S.player, res = S.res[p];
+__device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac) {
+    const int p = S.player, res = p ? S.res[1] : S.res[0];
     const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
               nbarracks = count_units(S, L, BARRACKS, true);
     for (int k = 0; k < S.n; k++) {   // bases
@@ -583,10 +591,11 @@ __device__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac
     };
     const int nf = count_where(S, L, own_worker);
     if (nf > 0) {
-        int reserved[4], nres = 0, used = 0, head = 0;   // head: workers taken off the free list
+        Rsv reserved{0, 0, 0};
+        int used = 0, head = 0;   // head: workers taken off the free list
         auto worker = [&](int idx) { return nth_where(S, L, idx, own_worker); };   // idx-th own worker, pgs.units order
         if (nbases == 0 && head < nf && res >= ut_cost(BASE) + used) {
-            build_if_not_already(S, L, worker(head++), BASE, reserved, nres);
+            build_if_not_already(S, L, worker(head++), BASE, reserved);
             used += ut_cost(BASE);
         }
         if (army == WORKER) {
@@ -594,7 +603,7 @@ __device__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac
             for (int k = head; k < nf; k++) melee_behavior(S, L, worker(k), po);
         } else {
             if (nbarracks == 0 && res >= ut_cost(BARRACKS) + used && head < nf) {
-                build_if_not_already(S, L, worker(head++), BARRACKS, reserved, nres);
+                build_if_not_already(S, L, worker(head++), BARRACKS, reserved);
                 used += ut_cost(BARRACKS);
             }
             if (coac) {
@@ -628,7 +637,7 @@ __device__ __forceinline__ void philox_b(uint32_t c[4], uint32_t k0, uint32_t k1
 // Unit.getUnitActions(gs, 10) enumerated in order on the bot's view.  Calls
 // f(code, weight) per action (weight 5 for attack / harvest / return).
 template <typename F>
-__device__ void unit_actions(const BS& S, const BL& L, int c, F f) {
+__device__ __forceinline__ void unit_actions(const BS& S, const BL& L, int c, F f) {
     const Grid gd{S.W, S.H, S.HW};
     const uint32_t u = L.unit[c];
     const int t = u_type(u), me = u_owner(u), ux = c % S.W, uy = c / S.W;
@@ -664,7 +673,7 @@ __device__ void unit_actions(const BS& S, const BL& L, int c, F f) {
     }
     const int prod = ut_produces(t);
     for (int pt = 0; pt < MRTS_NTYPES; pt++) {
-        if (!((prod >> pt) & 1) || S.res[me] < ut_cost(pt)) continue;
+        if (!((prod >> pt) & 1) || (me ? S.res[1] : S.res[0]) < ut_cost(pt)) continue;
         for (int d = 0; d < 4; d++)
             if (nb[d] >= 0 && !L.wall[nb[d]] && L.unit[nb[d]] == 0) f(code_make(A_PRODUCE, d, pt), 1);
     }
@@ -674,7 +683,7 @@ __device__ void unit_actions(const BS& S, const BL& L, int c, F f) {
     f(code_make(A_NONE, 10, 0), 1);
 }
 
-__device__ void random_biased_get_action(BS& S, const BL& L) {
+__device__ __forceinline__ void random_biased_get_action(BS& S, const BL& L) {
     // pa.ru starts as the usage of every pending assignment
     S.pa_res[0] = S.pend_res[0];
     S.pa_res[1] = S.pend_res[1];
@@ -802,7 +811,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         if (t != A_MOVE && t != A_PRODUCE) continue;
         RU r = usage(S, c, code, u_owner(L.unit[c]));
         atomicOr(&L.pend[(r.pos + W) >> 5], 1u << ((r.pos + W) & 31));
-        if (t == A_PRODUCE) atomicAdd(&L.sc[u_owner(L.unit[c])], r.res[u_owner(L.unit[c])]);
+        if (t == A_PRODUCE) atomicAdd(&L.sc[u_owner(L.unit[c])], u_owner(L.unit[c]) ? r.res[1] : r.res[0]);
     }
     // units in pgs.units order: ordered compaction by cell, then rank by uid
     int n = 0;

@@ -171,7 +171,6 @@ struct mrts_vec {
     EngineParams base{};
     // bot fusion (mrts_set_bot_fusion): k_step decides the next tick's bot actions
     int fuse = 1;             // requested
-    int fuse_cap = -1;        // resident workgroups of the fused k_step (-1: not yet asked)
     bool bots_ready = false;  // the bot decisions for the current state are in botpa / aa
 };
 
@@ -281,7 +280,6 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     if (((uintptr_t)dev & 255u) != 0) return fail(h, MRTS_EINVAL, "workspace must be 256-byte aligned");
     hipStream_t s = (hipStream_t)stream;
     h->bots_ready = false;
-    h->fuse_cap = -1;
     h->ws = (unsigned char *)dev;
     const int nm = (int)h->maps.size();
     std::vector<int4> mc((size_t)nm * h->HW);
@@ -336,14 +334,9 @@ static bool bound(mrts_vec *h) { return h && h->ws; }
 // decide for both sides: separate k_bot), to maps whose step workgroup has
 // waves besides the bot's (H*W > 64, the 64-lane workgroup of mrts_engine.hip's
 // dispatch), and when both LDS regions fit a workgroup.
-static bool fused(mrts_vec *h) {
-    if (!(h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && h->HW > 64 &&
-          mrts_engine_lds_bytes(h->HW, h->W) + 16 + mrts_engine_bot_lds_bytes(h->HW, h->W) <= 65536))
-        return false;
-    // only when every game's workgroup is resident at once (measured: coacAI 1024
-    // envs 13.0 -> 14.3 M env-steps/s fused; at 8192 envs fusion loses 15 %)
-    if (h->fuse_cap < 0) h->fuse_cap = mrts_engine_fused_capacity(&h->base);
-    return h->ngames <= h->fuse_cap;
+static bool fused(const mrts_vec *h) {
+    return h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && h->HW > 64 &&
+           mrts_engine_lds_bytes(h->HW, h->W) + 16 + mrts_engine_bot_lds_bytes(h->HW, h->W) <= 65536;
 }
 
 // k_bot (when the tick's bot decisions are not already there) + k_step on s

@@ -1273,6 +1273,7 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
 // ---------------------------------------------------------------------------
 // launchers
 
+#ifdef MRTS_STEP_PERSISTENT
 // Resident capacity of a kernel on the current device (blocks per CU x CUs),
 // cached per (kernel, LDS bytes, device).
 static int resident_blocks(const void* kernel, int NT, size_t sh) {
@@ -1291,6 +1292,7 @@ static int resident_blocks(const void* kernel, int NT, size_t sh) {
     cache.push_back({kernel, sh, dev, cus * per});
     return cus * per;
 }
+#endif
 
 template <typename K>
 static void launch_step(K kernel, int NT, size_t sh, hipStream_t s, const EngineParams& p) {
@@ -1389,24 +1391,6 @@ hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, in
     hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->HW, p->map_wall + (size_t)map * p->HW,
                        p->W, p->H, size, rgb);
     return hipGetLastError();
-}
-// Resident workgroups of the bot-fused k_step for this map on the current device
-// (0: no fused variant).  The host fuses only when every game's workgroup is
-// resident at once: with more games, the fused variant's occupancy (86 VGPRs,
-// step + bot LDS) costs more than the separate k_bot launch it saves.
-int mrts_engine_fused_capacity(const EngineParams* p) {
-    using namespace mrts;
-    if (p->HW <= 64) return 0;
-    const int NT = p->HW <= 128 ? 128 : 256;
-    const size_t sh = bots::b16(lds_bytes(p->HW, p->W, NT)) + bots::bot_lds_bytes(p->HW, p->W);
-    const void* k;
-    if (NT == 128)
-        k = p->partial_obs ? (p->obs_float ? (const void*)k_step<128, 31, float, true> : (const void*)k_step<128, 31, int32_t, true>)
-                           : (p->obs_float ? (const void*)k_step<128, 29, float, true> : (const void*)k_step<128, 29, int32_t, true>);
-    else
-        k = p->partial_obs ? (p->obs_float ? (const void*)k_step<256, 31, float, true> : (const void*)k_step<256, 31, int32_t, true>)
-                           : (p->obs_float ? (const void*)k_step<256, 29, float, true> : (const void*)k_step<256, 29, int32_t, true>);
-    return resident_blocks(k, NT, sh);
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {
     int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
