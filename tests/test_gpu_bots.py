@@ -187,3 +187,34 @@ def test_bot_fusion_with_map_cycling_and_resets():
     for e in envs:
         assert e.error_flags() == 0
         e.close()
+
+
+def test_bot_fusion_toggled_mid_game():
+    """mrts_set_bot_fusion switched on <-> off between steps: the decisions already made
+    by a fused step are used exactly once, so the run stays equal to the oracle."""
+    import torch
+
+    from gym_microrts import _native, microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv, sample_actions
+
+    ais = ["coacAI", "workerRushAI", "lightRushAI", "randomBiasedAI"]
+    w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    m = "maps/16x16/basesWorkers16x16.xml"
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=2, num_bot_envs=len(ais), max_steps=120, map_paths=[m], reward_weight=w,
+                               ai2s=[getattr(microrts_ai, a) for a in ais], return_tensors=True, obs_dtype=torch.int32)
+    o = OracleVecEnv(2, len(ais), [os.path.join(MAPS, m)], max_steps=120, ai2s=ais, reward_weight=w)
+    np.testing.assert_array_equal(g.reset().cpu().numpy(), o.reset())
+    for s in range(300):
+        if s % 37 == 0:
+            _native.check(_native.lib().mrts_set_bot_fusion(g._h, (s // 37) % 2), g._h, "set_bot_fusion")
+        mo = o.get_action_mask()
+        np.testing.assert_array_equal(g.get_action_mask().cpu().numpy(), mo, err_msg=f"mask step {s}")
+        a = sample_actions(mo, 5, s)
+        og, _, dg, _ = g.step(torch.from_numpy(a).to(g.device))
+        oo, _, do, _ = o.step(a)
+        np.testing.assert_array_equal(og.cpu().numpy(), oo, err_msg=f"obs step {s}")
+        np.testing.assert_array_equal(dg.cpu().numpy(), do, err_msg=f"done step {s}")
+    assert g.error_flags() == 0
+    g.close()
+    o.close()
