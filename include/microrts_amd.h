@@ -114,8 +114,8 @@ int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source);
  * wavefronts stream the observations and masks -- instead of a separate bot
  * kernel at the start of the next step; mrts_reset / mrts_reset_games decide
  * them for the games they reset.  Outputs are identical either way.  Applies
- * when no env has a bot as player 0 (MicroRTSBotVecEnv) and the map's two LDS
- * regions fit one workgroup; on = 0 launches the bot kernel at every step. */
+ * when no env has a bot as player 0 (MicroRTSBotVecEnv), the map has more than
+ * 64 cells and its two LDS regions fit one workgroup (160 KB); on = 0 launches the bot kernel at every step. */
 int mrts_set_bot_fusion(mrts_vec *h, int32_t on);
 
 /* step_async + JNIGridnetVecClient.gameStep (vec_env.py:968-984, 1002):
