@@ -132,15 +132,18 @@ def test_video_recorder_writes_frames(compat, tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(REF_PPO), reason="reference checkout only in the build container")
-def test_reference_ppo_gridnet_imports_unmodified(tmp_path):
-    """The unmodified experiments/ppo_gridnet.py gets through every import (gym,
-    stable_baselines3, torch.utils.tensorboard, gym_microrts = this package) and its
-    argument parser under the runner (the env itself needs the GPU)."""
+@pytest.mark.parametrize("script,flag", [("ppo_gridnet.py", "--num-selfplay-envs"), ("ppo_gridnet_eval.py", "--model-type"),
+                                         ("ppo_gridnet_large.py", "--num-selfplay-envs")])
+def test_reference_drivers_import_unmodified(tmp_path, script, flag):
+    """The unmodified experiments/ drivers get through every import
+    (gym, stable_baselines3, torch.utils.tensorboard, gym_microrts = this package) and their
+    argument parsers under the runner (the env itself needs the GPU)."""
     env = dict(os.environ, PYTHONPATH=PKG)
-    p = subprocess.run([sys.executable, "-m", "gym_microrts.run_driver", REF_PPO, "--help"], cwd=tmp_path, env=env,
+    path = os.path.join(os.path.dirname(REF_PPO), script)
+    p = subprocess.run([sys.executable, "-m", "gym_microrts.run_driver", path, "--help"], cwd=tmp_path, env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
-    assert "--num-selfplay-envs" in p.stdout and "--prior" in p.stdout
+    assert flag in p.stdout
 
 
 @pytest.mark.gpu
