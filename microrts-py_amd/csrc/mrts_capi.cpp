@@ -336,7 +336,7 @@ static bool bound(mrts_vec *h) { return h && h->ws; }
 // dispatch), and when both LDS regions fit a workgroup.
 static bool fused(const mrts_vec *h) {
     return h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && h->HW > 64 &&
-           mrts_engine_lds_bytes(h->HW, h->W) + 16 + mrts_engine_bot_lds_bytes(h->HW, h->W) <= 163840;
+           mrts_engine_fused_lds_bytes(h->HW, h->W) <= 163840;
 }
 
 // k_bot (when the tick's bot decisions are not already there) + k_step on s

@@ -49,5 +49,6 @@ hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n
 hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, int map, int size, uint8_t *rgb);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);
+size_t mrts_engine_fused_lds_bytes(int HW, int W);
 }
 #endif

@@ -88,6 +88,16 @@ __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     return b;
 }
 
+// Bot-fused k_step layout: [0, max(step, bot)) holds the step's arrays until
+// phase A's barrier and the bot's afterwards; the output words (one-hot + mask
+// bits, 32 B per cell for two views) get their own region behind it, so waves
+// 1.. can stream them while wave 0 reuses the rest.
+__host__ __device__ inline size_t fb_outw_offset(int HW, int W, int NT) {
+    const size_t a = lds_bytes(HW, W, NT), b = bots::bot_lds_bytes(HW, W);
+    return a16(a > b ? a : b);
+}
+__host__ __device__ inline size_t fb_lds_bytes(int HW, int W, int NT) { return fb_outw_offset(HW, W, NT) + a16(32 * (size_t)HW); }
+
 __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     Lds L;
     size_t o = 0;
@@ -661,6 +671,7 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
+    if (FB) L.outw = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
     const Grid gd{p.W, p.H, HW};
 #ifdef MRTS_EXP_FILL   // kernel-variant experiments only: zeros over one launch's output bytes, no loads
 #ifndef MRTS_EXP_FILL_SPLIT
@@ -985,7 +996,7 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
     const bool botg = FB && g >= p.nsp_games && NT > 64;
     emit_outputs<NT, P, OT>(p, L, G, kObs, kMasks && p.mask != nullptr, botg ? 64 : 0);
     if (FB && botg && threadIdx.x < 64)   // every read of the stored state is behind phase A's barrier
-        bots::bot_game<true>(p, g - p.nsp_games, 1, smem + bots::b16(lds_bytes(HW, p.W, NT)));
+        bots::bot_game<true>(p, g - p.nsp_games, 1, smem);   // the step's arrays are dead: only L.outw is read on
     __syncthreads();   // LDS is reused by the next game
     }
 }
@@ -1324,7 +1335,7 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
     } else if (p.fuse_bots && NT > 64) {
-        sh = bots::b16(sh) + bots::bot_lds_bytes(p.HW, p.W);
+        sh = fb_lds_bytes(p.HW, p.W, NT);
         if (p.partial_obs) {
             if (p.obs_float) launch_step(k_step<NT, 31, float, true>, NT, sh, s, p);
             else launch_step(k_step<NT, 31, int32_t, true>, NT, sh, s, p);
@@ -1391,6 +1402,10 @@ hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, in
     hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->HW, p->map_wall + (size_t)map * p->HW,
                        p->W, p->H, size, rgb);
     return hipGetLastError();
+}
+size_t mrts_engine_fused_lds_bytes(int HW, int W) {
+    const int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
+    return mrts::fb_lds_bytes(HW, W, NT);
 }
 size_t mrts_engine_lds_bytes(int HW, int W) {
     int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
