@@ -47,7 +47,8 @@ extern "C" {
 #define MRTS_AI_PO_LIGHT_RUSH 6
 #define MRTS_AI_PO_HEAVY_RUSH 7
 #define MRTS_AI_PO_RANGED_RUSH 8
-#define MRTS_AI_COUNT 9
+#define MRTS_AI_RANDOM 9 /* randomAI = ai.RandomBiasedSingleUnitAI (microrts_ai.py:7-10) */
+#define MRTS_AI_COUNT 10
 
 #define MRTS_OBS_INT32 0
 #define MRTS_OBS_FLOAT32 1

@@ -10,7 +10,8 @@
 //   workerRushAI, lightRushAI, POWorkerRush / POLightRush / POHeavyRush /
 //   PORangedRush (ai.abstraction.*: AbstractionLayerAI + Move / Harvest / Attack
 //   / Train / Build over breadth-first path finding), randomBiasedAI
-//   (ai.RandomBiasedAI on a counter-based Philox stream) and coacAI.
+//   (ai.RandomBiasedAI on a counter-based Philox stream), randomAI
+//   (ai.RandomBiasedSingleUnitAI) and coacAI.
 //
 // Mapping: one WAVEFRONT (64 lanes) per bot game.  The bot's decision logic is
 // inherently sequential (units in pgs.units order, the LinkedHashMap of
@@ -551,8 +552,8 @@ __device__ __forceinline__ int count_units(const BS& S, const BL& L, int type, b
     });
 }
 
-// WorkerRush / LightRush / HeavyRush / RangedRush (+ PO*), and coacAI
-__device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bool po, bool coac) {
+// WorkerRush / LightRush / HeavyRush / RangedRush (+ PO*)
+__device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bool po) {
     const int p = S.player, res = p ? S.res[1] : S.res[0];
     const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
               nbarracks = count_units(S, L, BARRACKS, true);
@@ -560,16 +561,11 @@ __device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bo
         const int c = L.ucell[k];
         const uint32_t u = L.unit[c];
         if (u_type(u) != BASE || u_owner(u) != p || L.act[c] != 0) continue;
-        bool tr;
-        if (army == WORKER) tr = res >= ut_cost(WORKER);
-        else if (coac) tr = nworkers < 2 * nbases + 2 && res >= ut_cost(WORKER);
-        else tr = nworkers < 1 && res >= ut_cost(WORKER);
+        const bool tr = army == WORKER ? res >= ut_cost(WORKER) : nworkers < 1 && res >= ut_cost(WORKER);
         if (tr) ab_train(S, L, L.uid[c], WORKER);
     }
     if (army != WORKER) {   // barracks
-        int t = army;
-        if (coac)
-            t = count_units(S, L, LIGHT, false) > count_units(S, L, RANGED, false) + count_units(S, L, HEAVY, false) ? HEAVY : RANGED;
+        const int t = army;
         for (int k = 0; k < S.n; k++) {
             const int c = L.ucell[k];
             const uint32_t u = L.unit[c];
@@ -606,18 +602,73 @@ __device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bo
                 build_if_not_already(S, L, worker(head++), BARRACKS, reserved);
                 used += ut_cost(BARRACKS);
             }
-            if (coac) {
-                const int nh = 2 * (nbases > 0 ? nbases : 1);
-                for (int k = head; k < nf; k++) {
-                    if (k - head < nh) harvest_behavior(S, L, worker(k));
-                    else melee_behavior(S, L, worker(k), po);
-                }
-            } else {
-                for (int k = head; k < nf; k++) harvest_behavior(S, L, worker(k));
-            }
+            for (int k = head; k < nf; k++) harvest_behavior(S, L, worker(k));
         }
     }
     BOT_STAMP(5);
+    translate_actions(S, L);
+}
+
+
+// coacAI: CoacAI's published strategy, restated (oracle/mrts_oracle_ai.c
+// coac_get_action; its free choices are fixed by league.db's outcomes)
+constexpr int COAC_HARVESTERS_PER_BASE = 2, COAC_EXTRA_WORKERS = 2, COAC_BARRACKS_MIN_WORKERS = 2, COAC_DEFENSE_RADIUS = 8;
+__device__ __forceinline__ void coac_get_action(BS& S, const BL& L) {
+    const int p = S.player, res = p ? S.res[1] : S.res[0];
+    const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
+              nbarracks = count_units(S, L, BARRACKS, true);
+    for (int k = 0; k < S.n; k++) {   // bases
+        const int c = L.ucell[k];
+        const uint32_t u = L.unit[c];
+        if (u_type(u) != BASE || u_owner(u) != p || L.act[c] != 0) continue;
+        if (nworkers < COAC_HARVESTERS_PER_BASE * nbases + COAC_EXTRA_WORKERS && res >= ut_cost(WORKER)) ab_train(S, L, L.uid[c], WORKER);
+    }
+    const int t = count_units(S, L, LIGHT, false) > count_units(S, L, RANGED, false) + count_units(S, L, HEAVY, false) ? HEAVY : RANGED;
+    for (int k = 0; k < S.n; k++) {   // barracks
+        const int c = L.ucell[k];
+        const uint32_t u = L.unit[c];
+        if (u_type(u) != BARRACKS || u_owner(u) != p || L.act[c] != 0) continue;
+        if (res >= ut_cost(t)) ab_train(S, L, L.uid[c], t);
+    }
+    for (int k = 0; k < S.n; k++) {   // army
+        const int c = L.ucell[k];
+        const uint32_t u = L.unit[c];
+        const int ty = u_type(u);
+        if (!ut_can_attack(ty) || ut_can_harvest(ty) || u_owner(u) != p || L.act[c] != 0) continue;
+        melee_behavior(S, L, c, false);
+    }
+    auto own_worker = [&](int c) {
+        const uint32_t u = L.unit[c];
+        return ut_can_harvest(u_type(u)) && u_owner(u) == p;
+    };
+    const int nf = count_where(S, L, own_worker);
+    if (nf > 0) {
+        Rsv reserved{0, 0, 0};
+        int used = 0, head = 0;
+        auto worker = [&](int idx) { return nth_where(S, L, idx, own_worker); };
+        if (nbases == 0 && head < nf && res >= ut_cost(BASE) + used) {
+            build_if_not_already(S, L, worker(head++), BASE, reserved);
+            used += ut_cost(BASE);
+        }
+        if (nbarracks == 0 && res >= ut_cost(BARRACKS) + used && head < nf && nworkers >= COAC_BARRACKS_MIN_WORKERS) {
+            build_if_not_already(S, L, worker(head++), BARRACKS, reserved);
+            used += ut_cost(BARRACKS);
+        }
+        const int nh = COAC_HARVESTERS_PER_BASE * (nbases > 0 ? nbases : 1);
+        for (int k = head; k < nf; k++) {
+            const int w = worker(k);
+            if (k - head < nh) {
+                harvest_behavior(S, L, w);
+                continue;
+            }
+            // defenders: the closest enemy when it is near the worker's closest own base
+            const int e = closest_enemy(S, L, w);
+            if (e < 0) continue;
+            const int b = closest_of(S, L, w, false);
+            if (b < 0 || iabs(b % S.W - e % S.W) + iabs(b / S.W - e / S.W) <= COAC_DEFENSE_RADIUS) ab_attack(S, L, L.uid[w], L.uid[e]);
+            else harvest_behavior(S, L, w);
+        }
+    }
     translate_actions(S, L);
 }
 
@@ -709,6 +760,37 @@ __device__ __forceinline__ void random_biased_get_action(BS& S, const BL& L) {
         if (consistent(S, r, L.pab, S.pa_res)) pa_add(S, L, c, pick);
         else pa_add(S, L, c, code_make(A_NONE, 10, 0));
     }
+}
+
+
+// RandomBiasedSingleUnitAI (randomAI): one unit acts at a time (oracle
+// random_single_get_action): nothing while a unit of the player is busy, else
+// one idle unit drawn uniformly gets a RandomBiasedAI-weighted action
+__device__ __forceinline__ void random_single_get_action(BS& S, const BL& L) {
+    auto own = [&](int c) { return u_owner(L.unit[c]) == S.player; };
+    if (count_where(S, L, [&](int c) { return own(c) && L.act[c] != 0; }) > 0) return;
+    const int ni = count_where(S, L, own);
+    if (ni == 0) return;
+    S.pa_res[0] = S.pend_res[0];
+    S.pa_res[1] = S.pend_res[1];
+    const int posw = (S.HW + 2 * S.W) / 32 + 1;
+    for (int i = threadIdx.x; i < posw; i += BT) L.pab[i] = L.pend[i];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    uint32_t ctr[4] = {0xFFFFFFFFu, S.tick, (uint32_t)S.game, 0x52534E47u + (uint32_t)(1 - S.player)};
+    philox_b(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
+    const int c = nth_where(S, L, (int)(((uint64_t)ctr[1] * (uint32_t)ni) >> 32), own);
+    int total = 0;
+    unit_actions(S, L, c, [&](int, int w) { total += w; });
+    int t = (int)(((uint64_t)ctr[0] * (uint32_t)total) >> 32), pick = -1;
+    unit_actions(S, L, c, [&](int code, int w) {
+        if (pick < 0) {
+            t -= w;
+            if (t < 0) pick = code;
+        }
+    });
+    if (pick < 0) pick = code_make(A_NONE, 10, 0);
+    RU r = usage(S, c, pick, S.player);
+    pa_add(S, L, c, consistent(S, r, L.pab, S.pa_res) ? pick : code_make(A_NONE, 10, 0));
 }
 
 // workgroup barrier of the one-wave k_bot; inside k_step only wave 0 runs the
@@ -872,7 +954,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     // the closest enemy of every unit (the scan closest_enemy would do, all
     // units at once; the state is fixed during getAction): L.pa[cell], staged
     // like the rows above (-1 = none)
-    for (int k = lane; S.ai != MRTS_AI_RANDOM_BIASED && k < n; k += BT) {
+    for (int k = lane; S.ai != MRTS_AI_RANDOM_BIASED && S.ai != MRTS_AI_RANDOM && k < n; k += BT) {
         const int cu = L.ucell[k], me = u_owner(L.unit[cu]), ux = cu % W, uy = cu / W;
         unsigned long long key = ~0ull;
         for (int j = 0; j < n; j++) {
@@ -888,14 +970,15 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     BOT_STAMP(4);
     switch (S.ai) {
-    case MRTS_AI_WORKER_RUSH: rush_get_action(S, L, WORKER, false, false); break;
-    case MRTS_AI_LIGHT_RUSH: rush_get_action(S, L, LIGHT, false, false); break;
-    case MRTS_AI_PO_WORKER_RUSH: rush_get_action(S, L, WORKER, true, false); break;
-    case MRTS_AI_PO_LIGHT_RUSH: rush_get_action(S, L, LIGHT, true, false); break;
-    case MRTS_AI_PO_HEAVY_RUSH: rush_get_action(S, L, HEAVY, true, false); break;
-    case MRTS_AI_PO_RANGED_RUSH: rush_get_action(S, L, RANGED, true, false); break;
-    case MRTS_AI_COAC: rush_get_action(S, L, RANGED, false, true); break;
+    case MRTS_AI_WORKER_RUSH: rush_get_action(S, L, WORKER, false); break;
+    case MRTS_AI_LIGHT_RUSH: rush_get_action(S, L, LIGHT, false); break;
+    case MRTS_AI_PO_WORKER_RUSH: rush_get_action(S, L, WORKER, true); break;
+    case MRTS_AI_PO_LIGHT_RUSH: rush_get_action(S, L, LIGHT, true); break;
+    case MRTS_AI_PO_HEAVY_RUSH: rush_get_action(S, L, HEAVY, true); break;
+    case MRTS_AI_PO_RANGED_RUSH: rush_get_action(S, L, RANGED, true); break;
+    case MRTS_AI_COAC: coac_get_action(S, L); break;
     case MRTS_AI_RANDOM_BIASED: random_biased_get_action(S, L); break;
+    case MRTS_AI_RANDOM: random_single_get_action(S, L); break;
     default: break;
     }
     bot_sync<FUSED>();

@@ -3,8 +3,8 @@
 In the reference each factory returns a Java AI object (`f(utt) -> AI`).  Here
 bots run on the device (mrts_bots.hip, one wavefront per bot game, launched
 before the step kernel), so a factory returns a descriptor naming the device
-bot.  Bots whose device implementation does not exist (randomAI, naiveMCTSAI
-and the competition bots other than coacAI) carry `ai_id = None` and make
+bot.  Bots whose device implementation does not exist (naiveMCTSAI and the
+competition bots other than coacAI) carry `ai_id = None` and make
 MicroRTSGridModeVecEnv raise NotImplementedError instead of silently
 substituting another policy.
 """
@@ -24,7 +24,7 @@ class DeviceAI:
 
 # ids match MRTS_AI_* in include/microrts_amd.h
 _IDS = {"passiveAI": 0, "workerRushAI": 1, "lightRushAI": 2, "randomBiasedAI": 3, "coacAI": 4,
-        "POWorkerRush": 5, "POLightRush": 6, "POHeavyRush": 7, "PORangedRush": 8}
+        "POWorkerRush": 5, "POLightRush": 6, "POHeavyRush": 7, "PORangedRush": 8, "randomAI": 9}
 
 
 def _factory(name):

@@ -46,7 +46,8 @@ typedef struct {
 
 /* AI ids for bot envs (gym_microrts/microrts_ai.py names). */
 enum { OAI_PASSIVE = 0, OAI_WORKER_RUSH = 1, OAI_LIGHT_RUSH = 2, OAI_RANDOM_BIASED = 3, OAI_COAC = 4,
-       OAI_PO_WORKER_RUSH = 5, OAI_PO_LIGHT_RUSH = 6, OAI_PO_HEAVY_RUSH = 7, OAI_PO_RANGED_RUSH = 8 };
+       OAI_PO_WORKER_RUSH = 5, OAI_PO_LIGHT_RUSH = 6, OAI_PO_HEAVY_RUSH = 7, OAI_PO_RANGED_RUSH = 8,
+       OAI_RANDOM = 9 };
 
 OVec *ovec_create(int num_selfplay, int num_bot, int max_steps, int partial_obs,
                   const OMap *maps, int num_maps, const int32_t *game_map,

@@ -19,8 +19,9 @@
  *   - RandomBiasedAI draws from a counter-based Philox stream keyed by
  *     (unit id, game tick, game) instead of an unseeded java.util.Random.
  *   - coacAI: CoacAI's strategy restated at the level of its published
- *     behaviour (economy of two harvesters per base, one barracks, ranged /
- *     heavy army chosen against the enemy composition, workers defend).
+ *     behaviour (coac_get_action), its free choices fixed by league.db's
+ *     bot-vs-bot outcomes.
+ *   - randomAI (RandomBiasedSingleUnitAI): one unit acting at a time.
  * The bot receives new PartiallyObservableGameState(gs, 1) under partial
  * observability (units it cannot observe are hidden), the full state otherwise,
  * and computes its PlayerAction before either player's actions of the tick are
@@ -499,6 +500,75 @@ static void rush_get_action(const OView *v, OAAMap *m, int army, int po, int coa
     translate_actions(v, m, pa);
 }
 
+
+/* ---- coacAI ------------------------------------------------------------------
+ * CoacAI (Coac.jar, vec_env.py:158; microrts_ai.py:58-61) restated at the level
+ * of its published strategy -- the jar is absent, so this is PARITY UNPINNED
+ * against Java and pinned only at the outcome level: the free choices below
+ * were fixed so that every bot-vs-bot outcome league.db records on
+ * basesWorkers16x16A (tests/golden/league_outcomes.json) is reproduced
+ * (DESIGN.md §4b):
+ *   - economy: each idle base trains a worker while the player owns fewer than
+ *     2 * bases + 2 workers; the first 2 * max(bases, 1) workers of the unit
+ *     list harvest (closest resource / closest base);
+ *   - one barracks, built once the player owns >= 2 workers (after a base
+ *     rebuild when no base is left); it trains ranged units, heavies when the
+ *     enemy fields more light units than ranged + heavy;
+ *   - army units attack the closest enemy;
+ *   - the remaining workers defend: attack the closest enemy when it is within
+ *     Manhattan distance 8 of the worker's closest own base, harvest otherwise. */
+enum { COAC_HARVESTERS_PER_BASE = 2, COAC_EXTRA_WORKERS = 2, COAC_BARRACKS_MIN_WORKERS = 2, COAC_DEFENSE_RADIUS = 8 };
+static int manh(const OUnit *a, const OUnit *b) { return absi(a->x - b->x) + absi(a->y - b->y); }
+static void coac_get_action(const OView *v, OAAMap *m, OPA *pa) {
+    const OGS *g = v->g;
+    const int p = v->player;
+    const int res = g->res[p];
+    int nworkers = count_own(v, T_WORKER), nbases = count_own(v, T_BASE), nbarracks = count_own(v, T_BARRACKS);
+    for (int i = 0; i < g->nu; i++) { /* bases */
+        const OUnit *u = &g->u[i];
+        if (!v_alive(v, i) || u->type != T_BASE || u->player != p || u->assign >= 0) continue;
+        if (nworkers < COAC_HARVESTERS_PER_BASE * nbases + COAC_EXTRA_WORKERS && res >= UT[T_WORKER].cost)
+            ab_train(m, i, T_WORKER);
+    }
+    const int t = count_enemy(v, T_LIGHT) > count_enemy(v, T_RANGED) + count_enemy(v, T_HEAVY) ? T_HEAVY : T_RANGED;
+    for (int i = 0; i < g->nu; i++) { /* barracks */
+        const OUnit *u = &g->u[i];
+        if (!v_alive(v, i) || u->type != T_BARRACKS || u->player != p || u->assign >= 0) continue;
+        if (res >= UT[t].cost) ab_train(m, i, t);
+    }
+    for (int i = 0; i < g->nu; i++) { /* army */
+        const OUnit *u = &g->u[i];
+        if (!v_alive(v, i) || !UT[u->type].can_attack || UT[u->type].can_harvest || u->player != p || u->assign >= 0)
+            continue;
+        melee_behavior(v, m, i, 0);
+    }
+    int free_w[MAX_HW_ORACLE], nf = 0; /* workers, busy ones included */
+    for (int i = 0; i < g->nu; i++)
+        if (v_alive(v, i) && UT[g->u[i].type].can_harvest && g->u[i].player == p) free_w[nf++] = i;
+    int reserved[8], nres = 0, used = 0, head = 0;
+    if (nbases == 0 && head < nf && res >= UT[T_BASE].cost + used) {
+        build_if_not_already(v, m, free_w[head++], T_BASE, reserved, &nres);
+        used += UT[T_BASE].cost;
+    }
+    if (nbarracks == 0 && res >= UT[T_BARRACKS].cost + used && head < nf && nworkers >= COAC_BARRACKS_MIN_WORKERS) {
+        build_if_not_already(v, m, free_w[head++], T_BARRACKS, reserved, &nres);
+        used += UT[T_BARRACKS].cost;
+    }
+    const int nh = COAC_HARVESTERS_PER_BASE * (nbases > 0 ? nbases : 1);
+    for (int k = head; k < nf; k++) {
+        const int w = free_w[k];
+        if (k - head < nh) {
+            harvest_behavior(v, m, w);
+            continue;
+        }
+        const int e = closest_enemy(v, w), b = closest_of(v, w, 0);
+        if (e < 0) continue;
+        if (b < 0 || manh(&g->u[b], &g->u[e]) <= COAC_DEFENSE_RADIUS) ab_attack(m, w, e);
+        else harvest_behavior(v, m, w);
+    }
+    translate_actions(v, m, pa);
+}
+
 /* ---- RandomBiasedAI.getAction --------------------------------------------- */
 static void random_biased_get_action(const OView *v, int game, uint32_t tick, OPA *pa) {
     /* stream per (unit, tick, game, player); player 1 keeps the 'RAND' tag */
@@ -542,6 +612,53 @@ static void random_biased_get_action(const OView *v, int game, uint32_t tick, OP
     }
 }
 
+/* ---- RandomBiasedSingleUnitAI (randomAI, microrts_ai.py:7-10) --------------------
+ * One unit acts at a time: while any unit of the player holds an action
+ * assignment the AI returns an empty PlayerAction; otherwise one idle unit,
+ * drawn uniformly, gets an action of getUnitActions(gs, 10) drawn with
+ * RandomBiasedAI's weights (5 for attack / harvest / return, 1 otherwise; the
+ * NONE(10) of the list when inconsistent).  Unseeded java.util.Random in Java;
+ * here Philox keyed by (tick, game) like randomBiasedAI.  Outcome-pinned by
+ * league.db (randomAI draws vs passiveAI, loses to every other bot). */
+static void random_single_get_action(const OView *v, int game, uint32_t tick, OPA *pa) {
+    const OGS *g = v->g;
+    const int p = v->player;
+    pa_init(pa);
+    int idle[MAX_HW_ORACLE], ni = 0;
+    for (int i = 0; i < g->nu; i++) {
+        if (!v_alive(v, i) || g->u[i].player != p) continue;
+        if (g->u[i].assign >= 0) return; /* a unit is still busy */
+        idle[ni++] = i;
+    }
+    if (ni == 0) return;
+    ORU r;
+    for (int i = 0; i < g->nu; i++) { /* reserved resources of the pending assignments */
+        if (!v_alive(v, i) || g->u[i].assign < 0) continue;
+        resource_usage(g, &g->u[i], &g->as[g->u[i].assign].act, &r);
+        ru_merge(&pa->ru, &r);
+        ru_free(&r);
+    }
+    uint32_t ctr[4] = {0xFFFFFFFFu, tick, (uint32_t)game, 0x52534E47u + (uint32_t)(1 - p)};
+    philox(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
+    const int i = idle[(int)(((uint64_t)ctr[1] * (uint32_t)ni) >> 32)];
+    OAct l[MAXLIST + 16];
+    const int n = unit_actions_h(g, v->hidden, i, 10, l);
+    int total = 0;
+    for (int k = 0; k < n; k++) total += (l[k].type == A_ATTACK || l[k].type == A_HARVEST || l[k].type == A_RETURN) ? 5 : 1;
+    int t = (int)(((uint64_t)ctr[0] * (uint32_t)total) >> 32), pick = n - 1;
+    for (int k = 0; k < n; k++) {
+        t -= (l[k].type == A_ATTACK || l[k].type == A_HARVEST || l[k].type == A_RETURN) ? 5 : 1;
+        if (t < 0) {
+            pick = k;
+            break;
+        }
+    }
+    resource_usage(g, &g->u[i], &l[pick], &r);
+    if (consistent_with(&r, &pa->ru, g)) pa_add(pa, i, &l[pick]);
+    else pa_add(pa, i, &l[n - 1]);
+    ru_free(&r);
+}
+
 /* ai.getAction(player, gs) for a bot game: ai2 for player 1 (bot envs), and
  * ai1 for player 0 in bot-vs-bot games (MicroRTSBotVecEnv, vec_env.py:1104-1236) */
 static void bot_get_action(const OGS *g, int ai, int player, int partial, int game, uint32_t tick, OAAMap *m, OPA *pa) {
@@ -559,8 +676,9 @@ static void bot_get_action(const OGS *g, int ai, int player, int partial, int ga
     case OAI_PO_LIGHT_RUSH: rush_get_action(&v, m, T_LIGHT, 1, 0, pa); break;
     case OAI_PO_HEAVY_RUSH: rush_get_action(&v, m, T_HEAVY, 1, 0, pa); break;
     case OAI_PO_RANGED_RUSH: rush_get_action(&v, m, T_RANGED, 1, 0, pa); break;
-    case OAI_COAC: rush_get_action(&v, m, T_RANGED, 0, 1, pa); break;
+    case OAI_COAC: coac_get_action(&v, m, pa); break;
     case OAI_RANDOM_BIASED: random_biased_get_action(&v, game, tick, pa); break;
+    case OAI_RANDOM: random_single_get_action(&v, game, tick, pa); break;
     default: passive_get_action((OGS *)g, player, pa); break;
     }
     free(hidden);

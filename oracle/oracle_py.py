@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmrts_oracle.so")
 UNIT_TYPES = ["Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"]
 AI_IDS = {"passiveAI": 0, "workerRushAI": 1, "lightRushAI": 2, "randomBiasedAI": 3, "coacAI": 4,
-          "POWorkerRush": 5, "POLightRush": 6, "POHeavyRush": 7, "PORangedRush": 8}
+          "POWorkerRush": 5, "POLightRush": 6, "POHeavyRush": 7, "PORangedRush": 8, "randomAI": 9}
 
 _lib = None
 

@@ -12,8 +12,8 @@ from conftest import MAPS
 from oracle_py import OracleVecEnv, sample_actions
 
 M16 = os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml")
-BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "POWorkerRush", "POLightRush", "POHeavyRush",
-        "PORangedRush"]
+BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "randomAI", "POWorkerRush", "POLightRush",
+        "POHeavyRush", "PORangedRush"]
 
 
 def rollout(ai, n, steps, partial_obs=False, seed=5, noop=False, map_path=M16, max_steps=2000):
@@ -66,7 +66,15 @@ def test_light_rush_builds_barracks_and_lights():
 def test_coac_builds_economy_and_barracks():
     r = rollout("coacAI", 2, 800, noop=True)
     assert any(_enemy_types(o)[2] > 0 for o in r["obs"])      # a barracks
-    assert max(_enemy_types(o)[3] for o in r["obs"]) >= 6      # 2 harvesters + defenders per base
+    assert max(_enemy_types(o)[3] for o in r["obs"]) >= 4      # 2 * bases + 2 workers
+    assert any(_enemy_types(o)[6] > 0 for o in r["obs"])      # ranged army
+
+
+def test_random_ai_one_unit_at_a_time():
+    """RandomBiasedSingleUnitAI: at most one of its units holds a non-NONE action"""
+    r = rollout("randomAI", 4, 400, noop=True)
+    acting = [int(((o[..., 12] == 1) & (o[..., 21] == 0)).sum(axis=(1, 2)).max()) for o in r["obs"]]
+    assert max(acting) <= 1 and sum(acting) > 0
 
 
 def test_worker_rush_trains_workers_and_wins_vs_passive():
@@ -90,24 +98,54 @@ def test_random_biased_acts():
     assert acting > 0
 
 
-def test_bot_vs_bot_outcomes_league_reference():
-    """MicroRTSBotVecEnv games of the restated bots on basesWorkers16x16A
-    (league.py:192, 236-245 setting, max_steps 5000).  league.db
-    records coacAI (p0) beating randomBiasedAI and passiveAI 5/5 -- reproduced
-    here.  Its coacAI-vs-workerRush / vs-lightRush outcomes are NOT reproduced by
-    the restated coacAI: outcome-level parity is partial."""
-    m = os.path.join(MAPS, "maps/16x16/basesWorkers16x16A.xml")
-    for a2 in ["randomBiasedAI", "passiveAI"]:
-        n = 5
-        e = OracleVecEnv(0, n, [m], max_steps=5000, ai2s=[a2] * n, ai1s=["coacAI"] * n)
-        e.reset()
-        res = [None] * n
-        for s in range(5000):
-            e.source_unit_mask = np.zeros((n, 256), np.int32)
-            r, d = e.step_raw(np.zeros((n, 256, 7), np.int64))
-            for k in np.nonzero(d[:, 0])[0]:
-                if res[k] is None:
-                    res[k] = int(r[k, 0])
-            if all(x is not None for x in res):
-                break
-        assert res == [1] * n, (a2, res)
+def league_outcomes():
+    import json
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "league_outcomes.json")) as f:
+        return json.load(f)
+
+
+def test_league_outcomes_reproduced_by_oracle():
+    """Every bot-vs-bot outcome the reference's league.db records (30 ordered pairs
+    among passive / randomBiased / random / lightRush / workerRush / coacAI, 5
+    matches each, MicroRTSBotVecEnv on basesWorkers16x16A with max_steps 5000:
+    league.py:236-245) is reproduced by the restated bots -- the only
+    reference-held evidence of how the Java bots play (tests/golden/
+    make_league_outcomes.py).  The device bots equal the oracle bit for bit
+    (tests/test_gpu_bots.py::test_league_outcomes_on_device)."""
+    L = league_outcomes()
+    pairs = [(q["p0"], q["p1"]) for q in L["pairs"]]
+    reps = 5
+    n = len(pairs) * reps
+    m = os.path.join(MAPS, L["map"])
+    e = OracleVecEnv(0, n, [m], max_steps=L["max_steps"], ai1s=[a for a, b in pairs for _ in range(reps)],
+                     ai2s=[b for a, b in pairs for _ in range(reps)])
+    e.reset()
+    res = [None] * n
+    for s in range(L["max_steps"]):
+        e.source_unit_mask = np.zeros((n, e.height * e.width), np.int32)
+        r, d = e.step_raw(np.zeros((n, e.height * e.width, 7), np.int64))
+        for k in np.nonzero(d[:, 0])[0]:
+            if res[k] is None:
+                res[k] = int(r[k, 0])
+        if all(x is not None for x in res):
+            break
+    e.close()
+    check_league(L, res, reps)
+
+
+RANDOM_BOTS = ("randomBiasedAI", "randomAI")   # unseeded java.util.Random in Java: outcomes vary per match
+
+
+def check_league(L, res, reps):
+    """deterministic pairs: the exact (win, draw, loss); pairs with a random bot:
+    the reference's majority outcome is ours too"""
+    for i, q in enumerate(L["pairs"]):
+        got = list(res[i * reps:(i + 1) * reps])
+        ref = [q["win"], q["draw"], q["loss"]]
+        wdl = [got.count(1), got.count(0), got.count(-1)]
+        if q["p0"] in RANDOM_BOTS or q["p1"] in RANDOM_BOTS:
+            mode = int(np.argmax(ref))
+            assert wdl[mode] * 2 > reps, (q, got)
+        else:
+            assert wdl == ref, (q, got)

@@ -11,8 +11,8 @@ from conftest import MAPS
 
 pytestmark = pytest.mark.gpu
 
-BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "POWorkerRush", "POLightRush", "POHeavyRush",
-        "PORangedRush"]
+BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "randomAI", "POWorkerRush", "POLightRush",
+        "POHeavyRush", "PORangedRush"]
 
 
 def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=2000, mode="masked", return_tensors=False,
@@ -63,7 +63,7 @@ def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=200
 @pytest.mark.parametrize("ai", BOTS)
 def test_bot_lockstep_16x16(ai, partial_obs):
     out = lockstep([ai] * 24, "maps/16x16/basesWorkers16x16.xml", 4, 700, partial_obs=partial_obs)
-    if ai in ("workerRushAI", "lightRushAI", "coacAI", "POWorkerRush", "POLightRush") and not partial_obs:
+    if ai in ("workerRushAI", "lightRushAI", "POWorkerRush", "POLightRush") and not partial_obs:
         assert out[0] > 0   # the faster rushes win some games against the random agent within 700 ticks
 
 
@@ -115,6 +115,48 @@ def test_bot_vs_bot_env_matches_oracle(partial_obs):
         np.testing.assert_array_equal(g._obs.cpu().numpy().astype(np.int32), o.encode(o.raw_obs()), err_msg=f"obs {s}")
         finished += int(do[:, 0].sum())
     assert finished > 12
+    assert g.error_flags() == 0
+
+
+def test_league_outcomes_on_device():
+    """league.db's 30 bot-vs-bot pairs (tests/golden/league_outcomes.json; 5 matches
+    each, basesWorkers16x16A, max_steps 5000: league.py:236-245) played by the
+    device bots through MicroRTSBotVecEnv, driven exactly as league.py's run_m2
+    (vec_env.py:1104-1236): every outcome matches the reference's record
+    (deterministic pairs exactly, pairs with a random bot by majority) and the
+    oracle's game for game."""
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSBotVecEnv
+    from oracle_py import OracleVecEnv
+    from test_bots_oracle import check_league, league_outcomes
+
+    L = league_outcomes()
+    reps = 5
+    ai1 = [q["p0"] for q in L["pairs"] for _ in range(reps)]
+    ai2 = [q["p1"] for q in L["pairs"] for _ in range(reps)]
+    n = len(ai1)
+    w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    g = MicroRTSBotVecEnv(ai1s=[getattr(microrts_ai, a) for a in ai1], ai2s=[getattr(microrts_ai, a) for a in ai2],
+                          map_paths=[L["map"]], max_steps=L["max_steps"], reward_weight=w)
+    o = OracleVecEnv(0, n, [os.path.join(MAPS, L["map"])], max_steps=L["max_steps"], ai2s=ai2, ai1s=ai1)
+    g.reset()
+    o.reset()
+    hw = g.height * g.width
+    res, ref = [None] * n, [None] * n
+    for s in range(L["max_steps"]):
+        _, _, dg, ig = g.step([[[0] * 8] * 2])   # run_m2's dummy actions (league.py:326-331)
+        o.source_unit_mask = np.zeros((n, hw), np.int32)
+        ro, do = o.step_raw(np.zeros((n, hw, 7), np.int64))
+        for k in np.nonzero(dg)[0]:
+            if res[k] is None:
+                res[k] = int(ig[k]["raw_rewards"][0])
+        for k in np.nonzero(do[:, 0])[0]:
+            if ref[k] is None:
+                ref[k] = int(ro[k, 0])
+        if all(x is not None for x in res):
+            break
+    assert res == ref
+    check_league(L, res, reps)
     assert g.error_flags() == 0
 
 
