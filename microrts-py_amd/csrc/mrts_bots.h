@@ -35,14 +35,6 @@ namespace bots {
 
 constexpr int BT = 64;   // one wavefront per bot game
 
-#ifdef MRTS_EXP_STAMPS   // kernel-variant experiments only: per-phase s_memtime stamps of k_bot
-constexpr int NSTAMP = 8, MAXSTAMPB = 16384;
-__device__ unsigned long long mrts_bot_stamps[MAXSTAMPB][NSTAMP];
-#define BOT_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < MAXSTAMPB && blockIdx.y == gridDim.y - 1) \
-    mrts_bot_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define BOT_STAMP(i) do { } while (0)
-#endif
 
 enum { AA_NONE = 0, AA_MOVE, AA_HARVEST, AA_ATTACK, AA_TRAIN, AA_BUILD };
 
@@ -247,9 +239,6 @@ __device__ __forceinline__ void pa_add(BS& S, const BL& L, int c, int code) {
 // the target) over free cells; the first layer that touches a free neighbour
 // of the start decides the move, ties UP, RIGHT, DOWN, LEFT.  -1 = null.
 __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
-#ifdef MRTS_EXP_NOPF   // kernel-variant experiments only: path finding skipped (behaviour changes)
-    return -1;
-#endif
     const int lane = threadIdx.x, sx = sc % S.W, sy = sc / S.W, r2 = range * range;
     if ((sx - tx) * (sx - tx) + (sy - ty) * (sy - ty) <= r2) return -1;
     const uint32_t rowmask = S.W == 32 ? 0xFFFFFFFFu : ((1u << S.W) - 1u);
@@ -605,7 +594,6 @@ __device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bo
             for (int k = head; k < nf; k++) harvest_behavior(S, L, worker(k));
         }
     }
-    BOT_STAMP(5);
     translate_actions(S, L);
 }
 
@@ -807,9 +795,6 @@ __device__ __forceinline__ void bot_sync() {
 
 
 // ---- the kernel ------------------------------------------------------------------------
-#ifndef MRTS_BOT_MIN_WAVES
-#define MRTS_BOT_MIN_WAVES 1
-#endif
 // ai.getAction(player, gs) of bot game b, by ONE wavefront (lanes = threadIdx.x
 // 0..63), LDS at `smem` (bot_lds_bytes).  FUSED: run by wave 0 of a k_step
 // workgroup for the NEXT tick while the other waves stream the outputs (no
@@ -829,7 +814,6 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         return;
     }
     BL L = bot_carve(smem, HW, W);
-    BOT_STAMP(0);
     int4* const aa_g = p.aa + ((size_t)b * 2 + player) * HW * 2;
     int32_t* const pa_g = p.botpa + ((size_t)b * 2 + player) * HW;
     S.W = W;
@@ -858,7 +842,6 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
     if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     bot_sync<FUSED>();
-    BOT_STAMP(1);
     // cells observable by the bot's player (PartiallyObservableGameState);
     // read only under partial observability (hidden units, PO* exploration)
     for (int c = lane; S.partial && c < HW; c += BT) {
@@ -885,7 +868,6 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         bot_sync<FUSED>();
     }
     // pending reservations of the visible units (isUnitActionAllowed)
-    BOT_STAMP(2);
     for (int c = lane; c < HW; c += BT) {
         const uint32_t a = L.act[c];
         if (a == 0) continue;
@@ -924,7 +906,6 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     }
     bot_sync<FUSED>();
     S.n = n;
-    BOT_STAMP(3);
     S.pend_res[0] = L.sc[0];
     S.pend_res[1] = L.sc[1];
     // lane y: free cells of row y, from one ballot per 64 cells (staged in L.pa,
@@ -968,7 +949,6 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         L.pa[cu] = key == ~0ull ? -1 : L.ucell[(int)(key & 0xFFFFFFFFu)];
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    BOT_STAMP(4);
     switch (S.ai) {
     case MRTS_AI_WORKER_RUSH: rush_get_action(S, L, WORKER, false); break;
     case MRTS_AI_LIGHT_RUSH: rush_get_action(S, L, LIGHT, false); break;
@@ -982,7 +962,6 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     default: break;
     }
     bot_sync<FUSED>();
-    BOT_STAMP(6);
     for (int i = lane; i < S.npa; i += BT) pa_g[i] = L.pa[i];
     for (int i = lane; i < 2 * S.naa; i += BT) aa_g[i] = L.aa[i];
     if (lane0()) {

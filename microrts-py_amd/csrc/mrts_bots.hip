@@ -14,7 +14,7 @@ namespace bots {
 // blockIdx.y = the bot's player: 1 = ai2 (every bot env), 0 = ai1 of a bot-vs-bot
 // game (MicroRTSBotVecEnv); both see the same pre-issue state.  With a game list
 // (p.bot_games), block i decides for game p.bot_games[i] if it is a bot game.
-__global__ __launch_bounds__(BT, MRTS_BOT_MIN_WAVES) void k_bot(EngineParams p) {
+__global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int player = gridDim.y == 2 ? (int)blockIdx.y : 1;
     int b = blockIdx.x;
@@ -37,11 +37,4 @@ hipError_t mrts_engine_bots(const EngineParams* p, hipStream_t s) {
     return hipGetLastError();
 }
 size_t mrts_engine_bot_lds_bytes(int HW, int W) { return mrts::bots::bot_lds_bytes(HW, W); }
-#ifdef MRTS_EXP_STAMPS
-int mrts_exp_bot_stamps(unsigned long long* out, int nblocks) {   // experiment builds only
-    const int n = nblocks < mrts::bots::MAXSTAMPB ? nblocks : mrts::bots::MAXSTAMPB;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mrts::bots::mrts_bot_stamps), sizeof(unsigned long long) * mrts::bots::NSTAMP * n)
-               ? -1 : n;
-}
-#endif
 }

@@ -63,14 +63,11 @@ static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // 16-byte store of an output row segment (obs / masks: written once, read by
-// the consumer after the kernel).  MRTS_NT_STORES selects non-temporal stores.
+// the consumer after the kernel; plain stores measured 5 % faster than
+// non-temporal ones)
 __device__ __forceinline__ void st16(void* dst, int a, int b, int c, int d) {
     v4i v = {a, b, c, d};
-#ifdef MRTS_NT_STORES
-    __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(dst));
-#else
     *reinterpret_cast<v4i*>(dst) = v;
-#endif
 }
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -283,6 +280,11 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
         }
     }
     __syncthreads();
+    // ---- phase B -----------------------------------------------------------
+    // Bot-fused k_step (skip = 64): from here on wave 0 runs bots::bot_game, whose
+    // LDS region starts at smem offset 0 and overwrites L.unit / uid / act / seq /
+    // aux / vis / sc.  Phase B must read nothing but the output words `ow` / `mw`
+    // (their own region at fb_outw_offset) and kernel parameters.
     if ((int)threadIdx.x < skip) return;
     const int t0 = (int)threadIdx.x - skip, nt = NT - skip;
     if (obs) {
@@ -448,35 +450,36 @@ __device__ __forceinline__ void issue_player(const EngineParams& p, const Lds& L
         int pos = -1, cost_new = 0;
         if (ctype == A_MOVE || ctype == A_PRODUCE) pos = nb_cell(gd, c, code_param(cur));
         if (ctype == A_PRODUCE) cost_new = ut_cost(code_utype(cur));
-        // uaa's inconsistent with the new ResourceUsage, in LinkedHashMap order
-        int cand[16];
-        int nc = 0;
-        if (pos >= 0 && L.resv[pos] >= 0) cand[nc++] = L.resv[pos];
+        // uaa's inconsistent with the new ResourceUsage (the holder of the target
+        // position, pending produces over a player's budget), visited in
+        // LinkedHashMap order: each pass takes the candidate of least issue
+        // sequence above the last one visited -- any number of candidates, no
+        // buffer.  Visiting a candidate rewrites only its own action, and every
+        // candidate is tested against its action before the visit, as in issue().
         const int nprod = L.sc[SC_NPROD];
-        for (int k = 0; k < nprod; k++) {
-            int pc = L.prod[k];
-            uint32_t pa = L.act[pc];
-            if (pa == 0 || code_type(act_code(pa)) != A_PRODUCE) continue;
-            int pp = u_owner(L.unit[pc]), cp = ut_cost(code_utype(act_code(pa)));
-            bool bad = false;
-            for (int pl = 0; pl < 2; pl++) {
-                int s = (pp == pl ? cp : 0) + (q == pl ? cost_new : 0);
-                if (s > 0 && s > res_of(L, pl)) bad = true;
-            }
-            if (!bad) continue;
-            bool dup = false;
-            for (int j = 0; j < nc; j++) dup |= cand[j] == pc;
-            if (!dup && nc < 16) cand[nc++] = pc;
-        }
-        for (int a = 1; a < nc; a++) {   // insertion sort by issue sequence
-            int x = cand[a];
-            int b = a - 1;
-            while (b >= 0 && L.seq[cand[b]] > L.seq[x]) { cand[b + 1] = cand[b]; b--; }
-            cand[b + 1] = x;
-        }
+        const int rc = (pos >= 0) ? L.resv[pos] : -1;
         bool original = true;
-        for (int k = 0; k < nc; k++) {
-            int cc = cand[k];
+        uint32_t last = 0;
+        for (bool first = true;; first = false) {
+            int cc = -1;
+            uint32_t best = 0xFFFFFFFFu;
+            if (rc >= 0 && (first || L.seq[rc] > last) && L.seq[rc] < best) { cc = rc; best = L.seq[rc]; }
+            for (int k = 0; k < nprod; k++) {
+                const int pc = L.prod[k];
+                const uint32_t sq = L.seq[pc];
+                if (pc == rc || (!first && sq <= last) || sq >= best) continue;
+                const uint32_t pa = L.act[pc];
+                if (pa == 0 || code_type(act_code(pa)) != A_PRODUCE) continue;
+                const int pp = u_owner(L.unit[pc]), cp = ut_cost(code_utype(act_code(pa)));
+                bool bad = false;
+                for (int pl = 0; pl < 2; pl++) {
+                    const int s = (pp == pl ? cp : 0) + (q == pl ? cost_new : 0);
+                    if (s > 0 && s > res_of(L, pl)) bad = true;
+                }
+                if (bad) { cc = pc; best = sq; }
+            }
+            if (cc < 0) break;
+            last = best;
             uint32_t ua = L.act[cc];
             if (seq_time(L.seq[cc]) == time) {    // CANCEL_BOTH
                 int ucode = act_code(ua);
@@ -647,72 +650,22 @@ __device__ __forceinline__ void commit_game(const EngineParams& p, const Lds& L,
     __syncthreads();
 }
 
-#ifndef MRTS_STEP_MIN_WAVES
-#define MRTS_STEP_MIN_WAVES 1
-#endif
-// blockIdx -> game.  MRTS_EXP_XCD (experiment): consecutive workgroups go to
-// the 8 XCDs round-robin; remap so each XCD steps a contiguous range of games.
-__device__ __forceinline__ int step_game_index(int G) {
-#ifdef MRTS_EXP_XCD
-    if ((G & 7) == 0 && (int)gridDim.x == G) return (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-#endif
-    return blockIdx.x;
-}
-// One game per workgroup.  MRTS_STEP_PERSISTENT (experiment): the grid is
-// sized to the resident capacity (launch_step) and block b steps games b,
-// b + gridDim.x, ..., prefetching the next game's state during the current
-// game's output stream (measured: hipcc's allocation of the looped body takes
-// 164 VGPRs, occupancy 3 -- DESIGN.md §5).
+// One game per workgroup (a persistent variant looping over games measured
+// slower: hipcc allocates 164 VGPRs for the looped body).
 // FB (bot fusion, p.fuse_bots): in a bot game's workgroup, wave 0 decides the
 // NEXT tick's bot actions (bots::bot_game on the state just stored) while waves
 // 1.. stream this tick's outputs; its LDS follows the step's (launch_all).
 template <int NT, int P, typename OT, bool FB = false>
-__global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p) {
+__global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
     if (FB) L.outw = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
     const Grid gd{p.W, p.H, HW};
-#ifdef MRTS_EXP_FILL   // kernel-variant experiments only: zeros over one launch's output bytes, no loads
-#ifndef MRTS_EXP_FILL_SPLIT
-#define MRTS_EXP_FILL_SPLIT 1
-#endif
-    {
-        const v4i z = {0, 0, 0, 0};
-        if (MRTS_EXP_FILL == 1) {   // per game: its envs' obs + mask rows (k_step's pattern)
-            const Game G = game_of(p, step_game_index(p.G));
-            v4i* o = reinterpret_cast<v4i*>(reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P);
-            for (int k = threadIdx.x; k < G.nviews * HW * P / 4; k += NT) o[k] = z;
-            v4i* m = reinterpret_cast<v4i*>(p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH);
-            for (int k = threadIdx.x; k < G.nviews * HW * MRTS_MASK_CH / 4; k += NT) m[k] = z;
-        } else if (MRTS_EXP_FILL == 3) {   // each game's rows split over MRTS_EXP_FILL_SPLIT blocks
-            const int part = blockIdx.x % MRTS_EXP_FILL_SPLIT;
-            const Game G = game_of(p, blockIdx.x / MRTS_EXP_FILL_SPLIT);
-            const int no = G.nviews * HW * P / 4, nm = G.nviews * HW * MRTS_MASK_CH / 4;
-            v4i* o = reinterpret_cast<v4i*>(reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P);
-            for (int k = part * no / MRTS_EXP_FILL_SPLIT + threadIdx.x; k < (part + 1) * no / MRTS_EXP_FILL_SPLIT; k += NT) o[k] = z;
-            v4i* m = reinterpret_cast<v4i*>(p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH);
-            for (int k = part * nm / MRTS_EXP_FILL_SPLIT + threadIdx.x; k < (part + 1) * nm / MRTS_EXP_FILL_SPLIT; k += NT) m[k] = z;
-        } else {                    // grid-stride over both arrays (a fill kernel's pattern)
-            const long long N = p.nsp + (p.G - p.nsp_games), st = (long long)gridDim.x * NT;
-            v4i* o = reinterpret_cast<v4i*>(p.obs);
-            for (long long k = (long long)blockIdx.x * NT + threadIdx.x; k < N * HW * P / 4; k += st) o[k] = z;
-            v4i* m = reinterpret_cast<v4i*>(p.mask);
-            for (long long k = (long long)blockIdx.x * NT + threadIdx.x; k < N * HW * MRTS_MASK_CH / 4; k += st) m[k] = z;
-        }
-        return;
-    }
-#endif
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
-#ifdef MRTS_STEP_PERSISTENT
-    if (pf_ok && (int)blockIdx.x < p.G) prefetch_game<NT>(p, blockIdx.x, pf);
-    for (int g = blockIdx.x; g < p.G; g += gridDim.x) {
-#else
-    const int g = step_game_index(p.G);
+    const int g = blockIdx.x;
     if (pf_ok) prefetch_game<NT>(p, g, pf);
-    {
-#endif
     const Game G = game_of(p, g);
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
     // the source-unit rows of this lane's first cell, fetched in the same round
@@ -727,7 +680,6 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
     __syncthreads();
     if (pf_ok) commit_game<NT>(p, L, pf);
     else load_game<NT>(p, L, g);
-#ifndef MRTS_EXP_NOLOGIC   // kernel-variant experiments only: state in, outputs out, no game logic
     const int time = L.sc[SC_TIME];
     // bot-vs-bot game (MicroRTSBotVecEnv): player 0's PlayerAction comes from k_bot too
     const bool bot0 = !G.selfplay && p.bot_ai0 && p.bot_ai0[g - p.nsp_games] >= 0;
@@ -974,31 +926,14 @@ __global__ __launch_bounds__(NT, MRTS_STEP_MIN_WAVES) void k_step(EngineParams p
         L.sc[SC_STEPS] = steps;
     }
     __syncthreads();
-#endif
-#ifdef MRTS_STEP_PERSISTENT
-    // the next game's state: in flight while this game's outputs stream out
-    if (pf_ok && g + (int)gridDim.x < p.G) prefetch_game<NT>(p, g + gridDim.x, pf);
-#endif
     // (7) write back + one-hot observation of every view
     store_game<NT>(p, L, g);
     // + getMasks of the next tick (bound mask outputs): every read of this
     //   game's source rows (phase 1) is behind the barriers above
-#ifdef MRTS_EXP_NOOBS   // kernel-variant experiments only (scripts/kernel_variants.py)
-    constexpr bool kObs = false;
-#else
-    constexpr bool kObs = true;
-#endif
-#ifdef MRTS_EXP_NOMASKW
-    constexpr bool kMasks = false;
-#else
-    constexpr bool kMasks = true;
-#endif
     const bool botg = FB && g >= p.nsp_games && NT > 64;
-    emit_outputs<NT, P, OT>(p, L, G, kObs, kMasks && p.mask != nullptr, botg ? 64 : 0);
+    emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0);
     if (FB && botg && threadIdx.x < 64)   // every read of the stored state is behind phase A's barrier
         bots::bot_game<true>(p, g - p.nsp_games, 1, smem);   // the step's arrays are dead: only L.outw is read on
-    __syncthreads();   // LDS is reused by the next game
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1115,10 +1050,7 @@ __device__ __forceinline__ void sample_row(uint64_t lo, uint64_t hi, int e, int 
 // selection arithmetic.  The 7 int64 components per row are staged in LDS and
 // written back with coalesced 16-byte stores.  No block barriers: a wave's own
 // LDS operations complete in order.
-#ifndef MRTS_SAMPLE_ROWS
-#define MRTS_SAMPLE_ROWS 32
-#endif
-constexpr int SW = MRTS_SAMPLE_ROWS;                     // rows per group (one wave)
+constexpr int SW = 32;                                   // rows per group (one wave)
 constexpr int SWAVES = 4;                                // waves per workgroup
 constexpr int SNV = (SW * MRTS_MASK_CH / 4 + 63) / 64;   // dwordx4 loads per lane per group (10)
 
@@ -1190,13 +1122,8 @@ __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* 
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
-#ifndef MRTS_SAMPLE_MIN_WAVES
-#define MRTS_SAMPLE_MIN_WAVES 1
-#endif
-#ifndef MRTS_SAMPLE_BLOCKS_PER_CU
-#define MRTS_SAMPLE_BLOCKS_PER_CU 16   // measured best (scripts/kernel_variants.py: 2 -> 151 us, 4 -> 138, 8 -> 133, 16 -> 127, 64 -> 178)
-#endif
-__global__ __launch_bounds__(64 * SWAVES, MRTS_SAMPLE_MIN_WAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
+constexpr int SAMPLE_BLOCKS_PER_CU = 16;   // measured best (round 1: 2 -> 151 us, 4 -> 138, 8 -> 133, 16 -> 127, 64 -> 178)
+__global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
                                                         uint32_t step, int64_t* __restrict__ act) {
     __shared__ uint32_t s_bits[SWAVES][SW * 3];
     __shared__ __attribute__((aligned(16))) int64_t s_out[SWAVES][SW * 7];
@@ -1284,38 +1211,10 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
 // ---------------------------------------------------------------------------
 // launchers
 
-#ifdef MRTS_STEP_PERSISTENT
-// Resident capacity of a kernel on the current device (blocks per CU x CUs),
-// cached per (kernel, LDS bytes, device).
-static int resident_blocks(const void* kernel, int NT, size_t sh) {
-    struct Entry { const void* k; size_t sh; int dev, blocks; };
-    static std::mutex mu;
-    static std::vector<Entry> cache;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::lock_guard<std::mutex> lock(mu);
-    for (const Entry& e : cache)
-        if (e.k == kernel && e.sh == sh && e.dev == dev) return e.blocks;
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, NT, sh) != hipSuccess)
-        return 0;
-    cache.push_back({kernel, sh, dev, cus * per});
-    return cus * per;
-}
-#endif
 
 template <typename K>
 static void launch_step(K kernel, int NT, size_t sh, hipStream_t s, const EngineParams& p) {
-    int grid = p.G;
-#ifdef MRTS_EXP_FILL_SPLIT
-    grid *= MRTS_EXP_FILL_SPLIT;
-#endif
-#ifdef MRTS_STEP_PERSISTENT
-    const int cap = resident_blocks(reinterpret_cast<const void*>(kernel), NT, sh);
-    if (cap > 0) grid = std::min(grid, cap);
-#endif
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(NT), sh, s, p);
+    hipLaunchKernelGGL(kernel, dim3(p.G), dim3(NT), sh, s, p);
 }
 
 template <int NT>
@@ -1356,9 +1255,6 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
 }
 
 static hipError_t dispatch(const EngineParams& p, int kind, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
-#ifdef MRTS_FORCE_NT   // kernel-variant experiments only: workgroup size independent of the map
-    return launch_all<MRTS_FORCE_NT>(p, kind, s, games, maps, count);
-#endif
     if (p.HW <= 64) return launch_all<64>(p, kind, s, games, maps, count);
     if (p.HW <= 128) return launch_all<128>(p, kind, s, games, maps, count);
     return launch_all<256>(p, kind, s, games, maps, count);
@@ -1385,7 +1281,7 @@ hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed,
     if (total == 0) return hipSuccess;
     // persistent grid: enough waves to keep every CU streaming, each looping over row groups
     const long long groups = ((long long)total + mrts::SW - 1) / mrts::SW;
-    const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * MRTS_SAMPLE_BLOCKS_PER_CU);   // resident blocks
+    const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * mrts::SAMPLE_BLOCKS_PER_CU);   // resident blocks
     hipLaunchKernelGGL(mrts::k_sample, dim3((unsigned)blocks), dim3(64 * mrts::SWAVES), 0, s, mask, n, hw, seed, step, act);
     return hipGetLastError();
 }

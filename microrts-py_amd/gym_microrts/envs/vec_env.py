@@ -86,6 +86,7 @@ class LazyInfos:
 
 class MicroRTSGridModeVecEnv:
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 150}
+    _cycle_min = 0   # map cycling when len(cycle_maps) > _cycle_min (vec_env.py:1038)
 
     class PriorMode(Enum):
         """vec_env.py:48-84.  Only NONE is supported (the KG prior is out of
@@ -227,8 +228,7 @@ class MicroRTSGridModeVecEnv:
             self._rew = torch.zeros((self.num_envs,), dtype=torch.float64, device=self.device)
             self._done0 = torch.zeros((self.num_envs,), dtype=torch.bool, device=self.device)
         _native.check(_native.lib().mrts_bind_workspace(self._h, self._ws.data_ptr(), self._stream()), self._h, "bind_workspace")
-        rw = np.ascontiguousarray(np.asarray(reward_weight, dtype=np.float64).reshape(6))
-        _native.check(_native.lib().mrts_set_reward_weight(self._h, rw.ctypes.data, int(bool(reward_shaping))), self._h, "set_reward_weight")
+        self.reward_weight = reward_weight   # the setter sends it to the engine
         # eager masks: reset / step / map-cycling resets also write getMasks(0) of
         # the state they leave (mrts_bind_mask_outputs), in the same kernel pass, so
         # get_action_mask() after them launches nothing (the rollout loop calls it
@@ -259,6 +259,21 @@ class MicroRTSGridModeVecEnv:
         self.kernel_events = None
 
     # ------------------------------------------------------------------ utils
+    @property
+    def reward_weight(self):
+        return self._reward_weight
+
+    @reward_weight.setter
+    def reward_weight(self, w):
+        """vec_env.py:1057 reads self.reward_weight on every step_wait; the tensor
+        path's fused `raw @ w` reads the engine's copy, so a reassignment is sent
+        to the engine at once."""
+        self._reward_weight = w
+        if getattr(self, "_h", None):
+            rw = np.ascontiguousarray(np.asarray(w, dtype=np.float64).reshape(6))
+            _native.check(_native.lib().mrts_set_reward_weight(self._h, rw.ctypes.data, int(bool(self.reward_shaping))), self._h,
+                          "set_reward_weight")
+
     def _launch(self, name, fn, *args):
         ev = self.kernel_events
         if ev is None:
@@ -331,7 +346,7 @@ class MicroRTSGridModeVecEnv:
             if not self.reward_shaping:
                 raw = raw.clone()
                 raw[:, 1:] = 0
-            if len(self.cycle_maps) > 0:
+            if len(self.cycle_maps) > self._cycle_min:
                 self._cycle(self._done0.cpu().numpy())
             return self._obs, self._rew, self._done0, LazyInfos(raw)
         self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
@@ -340,7 +355,7 @@ class MicroRTSGridModeVecEnv:
         done = self._done.cpu().numpy().astype(bool)
         if not self.reward_shaping:
             reward[:, 1:] = 0
-        if len(self.cycle_maps) > 0:
+        if len(self.cycle_maps) > self._cycle_min:
             self._cycle(done[:, 0])
         obs = self._obs.cpu().numpy()
         infos = [{"raw_rewards": item} for item in reward]
@@ -483,7 +498,10 @@ class MicroRTSGridModeSharedMemVecEnv(MicroRTSGridModeVecEnv):
     `raw @ reward_weight` in numpy, dones `done[:, 0]`, infos `[{"raw_rewards": r}]`.
     The reference forwards its arguments to the base class by position, which
     shifts `reward_weight` into `reward_shaping`; they are
-    forwarded by name here."""
+    forwarded by name here.  It cycles maps only with more than one cycle map
+    (vec_env.py:1344), not with one as the base class (vec_env.py:1038)."""
+
+    _cycle_min = 1
 
     def __init__(
         self,

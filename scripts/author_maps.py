@@ -109,6 +109,11 @@ def main():
     # reference default map (vec_env.py:95)
     write_map("10x10/basesTwoWorkers10x10.xml", 10, 10,
               [R(0, 0), R(9, 9), B(0, 2, 2), B(1, 7, 7), W(0, 1, 1), W(0, 2, 1), W(1, 8, 8), W(1, 7, 8)])
+    # 32x32: the largest map the engine takes (fused bot LDS > 64 KB)
+    write_map("32x32/basesWorkers32x32.xml", 32, 32, bases_workers(32))
+    # 40 barracks for player 0 (issue()'s pending-produce candidates beyond 16)
+    field = [("Barracks", 0, x, y, 0, 4) for y in (1, 4, 7, 10, 13) for x in range(0, 16, 2)]
+    write_map("16x16/barracksField16x16.xml", 16, 16, field + [B(1, 15, 15), W(1, 15, 14)], res=(40, 5))
     # barricades: wall at (6,6) pinned, the rest authored (point symmetric)
     walls = []
     for k in range(6, 10):

@@ -345,3 +345,60 @@ def test_no_invariant_violation_long_run():
     torch.cuda.synchronize()
     assert g.error_flags() == 0
     assert (obs.sum(-1) == 6).all()
+
+
+def test_issue_many_inconsistent_pending_produces():
+    """issue()'s candidate walk with more than 16 inconsistent pending assignments
+    (the walk had a 16-entry buffer).  On barracksField16x16 player 0
+    queues 18 heavies (tick 0) and 20 lights (tick 1) against 40 resources -- the
+    pairwise ResourceUsage test admits both batches -- the lights complete first
+    (tick 81) and leave 0 resources while the 18 heavies are still pending, so from
+    then on every new action of player 0 meets 18 over-budget produces.  GPU ==
+    oracle every tick, with masked random actions for every other row."""
+    from oracle_py import sample_actions
+
+    m = "maps/16x16/barracksField16x16.xml"
+    g = make_gpu_env(2, 0, m, 2000)
+    o = make_oracle(2, 0, m, 2000)
+    np.testing.assert_array_equal(g.reset(), o.reset())
+    cells = [y * 16 + x for y in (1, 4, 7, 10, 13) for x in range(0, 16, 2)]
+    worst = 0
+    for t in range(160):
+        mg, mo = g.get_action_mask(), o.get_action_mask()
+        np.testing.assert_array_equal(mg, mo, err_msg=f"mask {t}")
+        a = sample_actions(mo, 11, t)
+        if t < 2:
+            a[:] = 0
+            for c in (cells[:18] if t == 0 else cells[18:38]):
+                a[0, c] = [4, 0, 0, 0, 2, 5 if t == 0 else 4, 0]
+        og, rg, dg, ig = g.step(a)
+        oo, ro, do, io = o.step(a)
+        np.testing.assert_array_equal(og, oo, err_msg=f"obs {t}")
+        np.testing.assert_array_equal(rg, ro, err_msg=f"reward {t}")
+        np.testing.assert_array_equal(dg, do)
+        d = o.dump_cells(0)
+        res0 = o.game_resources(0)[0]
+        over = int(((d[:, 1] == 0) & (d[:, 4] == 4) & (res0 < 2)).sum())
+        worst = max(worst, over)
+    assert worst > 16, worst
+    assert g.error_flags() == 0
+
+
+def test_reward_weight_reassigned_mid_run():
+    """vec_env.py:1057 reads self.reward_weight every step: a reassignment after
+    construction reaches the tensor path's fused `raw @ w`."""
+    from oracle_py import sample_actions
+
+    torch = _torch()
+    g = make_gpu_env(16, 4, "maps/16x16/basesWorkers16x16.xml", 300, return_tensors=True)
+    o = make_oracle(16, 4, "maps/16x16/basesWorkers16x16.xml", 300)
+    g.reset()
+    o.reset()
+    for s in range(120):
+        if s == 40:
+            g.reward_weight = o.reward_weight = np.array([1.0, 2.0, 3.0, 0.5, 7.0, 11.0])
+        mo = o.get_action_mask()
+        a = sample_actions(mo, 3, s)
+        _, rg, _, _ = g.step(torch.from_numpy(a).to(g.device))
+        _, ro, _, _ = o.step(a)
+        np.testing.assert_allclose(rg.cpu().numpy(), ro, rtol=0, atol=1e-12, err_msg=f"step {s}")
