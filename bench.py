@@ -56,6 +56,15 @@ def parse():
                     help="src: mrts_sample_actions_src (reads the mask rows of source cells only); dense: every row")
     ap.add_argument("--workload", default="selfplay", choices=sorted(WORKLOADS),
                     help="selfplay = the BASELINE metric; the others are the secondary BASELINE.json configs")
+    ap.add_argument("--preroll", type=int, default=-1,
+                    help="untimed ticks played before --warmup with staggered game resets, so the timed window sees "
+                         "games at every phase of an episode (mid-game states, gameovers, auto-resets); "
+                         "-1 = max_steps, 0 = off (every game starts fresh at the first warmup step)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group of the timing barrier / max-over-ranks (nccl = RCCL; gloo lets several ranks "
+                         "share one GPU, as tests/test_gpu_shard.py does)")
+    ap.add_argument("--dump", default=None,
+                    help="save each rank's final obs / masks / raw rewards / dones to DUMP.rank<r>.npz (shard tests)")
     return ap.parse_args()
 
 
@@ -74,6 +83,47 @@ WORKLOADS = {
 # configs[4]: mixed sizes bucketed in one batch; per bucket (map, selfplay envs, bot envs per bot kind)
 MIXED = [("maps/8x8/basesWorkers8x8.xml", 0.25), ("maps/16x16/basesWorkers16x16.xml", 0.5),
          ("maps/24x24/basesWorkers24x24.xml", 0.25)]
+
+
+def stagger_plan(G, ticks, game0=0, G_total=None):
+    """Global game g of G_total is reset at pre-roll tick floor(g * ticks / G_total):
+    after `ticks` ticks the games' episode ages spread evenly over (0, ticks]
+    (time-limit resets then fall at every tick of the timed window, not all at
+    once).  A shard holds global games [game0, game0 + G); returns its local
+    indices per tick, so shards reset exactly the games one unsharded run would."""
+    G_total = G if G_total is None else G_total
+    plan = [[] for _ in range(ticks)]
+    for g in range(G):
+        plan[(game0 + g) * ticks // G_total].append(g)
+    return plan
+
+
+def preroll(envs, one_step, ticks, rank=0, world=1):
+    """`ticks` untimed steps of the bench loop; each env resets its share of games
+    at staggered ticks (stagger_plan; every rank holds an equal slice of the global
+    games).  Returns the number of ticks played."""
+    plans = [stagger_plan(e._n_games(), ticks, rank * e._n_games(), world * e._n_games()) for e in envs]
+    for s in range(ticks):
+        one_step(s)
+        for e, plan in zip(envs, plans):
+            e.reset_games(plan[s])
+    return ticks
+
+
+def window_stats(before, after, steps):
+    """What the timed window covered, from mrts_game_stats before / after it:
+    episode phase (game time) at its start and end, auto-resets, and the serial
+    one-lane work (ordered execution ticks, ordered-path issue rows)."""
+    import numpy as np
+
+    b, a = np.concatenate(before), np.concatenate(after)
+    G = a.shape[0]
+    return {"games": int(G),
+            "game_tick_start": {"min": int(b[:, 0].min()), "mean": round(float(b[:, 0].mean()), 1), "max": int(b[:, 0].max())},
+            "game_tick_end": {"min": int(a[:, 0].min()), "mean": round(float(a[:, 0].mean()), 1), "max": int(a[:, 0].max())},
+            "auto_resets": int((a[:, 5] - b[:, 5]).sum()),
+            "serial_exec_games_per_step": round(float((a[:, 3] - b[:, 3]).sum()) / steps, 1),
+            "ordered_issue_rows_per_step": round(float((a[:, 4] - b[:, 4]).sum()) / steps, 1)}
 
 
 def run_mixed(args, rank, dev):
@@ -96,24 +146,46 @@ def run_mixed(args, rank, dev):
                                  reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), eager_masks=not args.no_eager_masks)
     lib = _native.lib()
     acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=dev) for e in env.envs]
-    seed = (args.seed << 32) | rank
+    seed = args.seed
+    ev = {}
+    timing = [False]
 
     def one_step(s):
         masks = env.get_action_mask()
+        rec = timing[0] and s % args.event_every == 0
         for e, m, a in zip(env.envs, masks, acts):
-            _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, seed, s, a), None, "sample")
+            e.kernel_events = ev.setdefault(e.height, {}) if rec else None
+            _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, rank * e.num_envs,
+                                 seed, s, a), None, "sample")
         return env.step(acts)
 
     env.reset()
-    for s in range(args.warmup):
+    s0 = preroll(env.envs, one_step, args.max_steps if args.preroll < 0 else args.preroll, rank,
+                 int(os.environ.get("WORLD_SIZE", "1")))
+    for s in range(s0, s0 + args.warmup):
         one_step(s)
     torch.cuda.synchronize()
+    before = [e.game_stats() for e in env.envs]
+    timing[0] = not args.no_kernel_events
     t0 = time.perf_counter()
-    for s in range(args.warmup, args.warmup + args.steps):
+    for s in range(s0 + args.warmup, s0 + args.warmup + args.steps):
         one_step(s)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    return elapsed, {}, env.error_flags(), 256, sum(e.num_envs for e in env.envs) // 2, env.num_envs, 29, 0
+    for e in env.envs:
+        e.kernel_events = None
+    after = [e.game_stats() for e in env.envs]
+    # per bucket: mean step-kernel launch time and its algorithmic bytes
+    buckets = []
+    for e in env.envs:
+        hw, G = e.height * e.width, e._n_games()
+        kb = kernel_bytes(G, e.num_envs, hw, sum(e.num_planes))
+        k = {name: float(np.mean([a.elapsed_time(b) for a, b in v])) for name, v in ev.get(e.height, {}).items()}
+        buckets.append({"map": f"{e.height}x{e.width}", "envs": e.num_envs, "games": G, "step_ms": k.get("step"),
+                        "step_bytes": kb["step"]})
+    stats = window_stats(before, after, args.steps)
+    stats["buckets"] = buckets
+    return elapsed, {}, env.error_flags(), 256, sum(e._n_games() for e in env.envs), env.num_envs, 29, 0, stats
 
 
 WORKLOAD_DESC = {
@@ -128,22 +200,28 @@ WORKLOAD_DESC = {
 }
 
 
-def sample(lib, kind, mask, source, n, hw, seed, step, act):
+def sample(lib, kind, mask, source, n, hw, env0, seed, step, act):
     """The bench's stand-in policy: a uniform pick among the valid entries of
-    every component of every cell (hello_world.py:27-64), on the device."""
+    every component of every cell (hello_world.py:27-64), on the device; env0 =
+    the global index of the shard's first env (Philox counter)."""
     import torch
 
     st = torch.cuda.current_stream().cuda_stream
     if kind == "src":
-        return lib.mrts_sample_actions_src(st, mask.data_ptr(), source.data_ptr(), n, hw, seed, step, act.data_ptr())
-    return lib.mrts_sample_actions(st, mask.data_ptr(), n, hw, seed, step, act.data_ptr())
+        return lib.mrts_sample_actions_src(st, mask.data_ptr(), source.data_ptr(), n, hw, env0, seed, step, act.data_ptr())
+    return lib.mrts_sample_actions(st, mask.data_ptr(), n, hw, env0, seed, step, act.data_ptr())
 
 
-def shard(rank, n):
-    """rank r owns global envs [r*n, (r+1)*n); n even so selfplay pairs never straddle
-    ranks; the sampler seed is shard-specific."""
+def shard(rank, n, nsp, nbot):
+    """rank r owns global envs [r*n, (r+1)*n) of one batch of world*n envs: its
+    selfplay envs / bot envs are that slice of the global selfplay / bot envs.
+    Returns (env0, game_offset): the sampler's global env index of the shard's
+    first env and the global index of its first game (bot RNG streams), so
+    shard r plays exactly the games of that slice of one unsharded run.  n even:
+    selfplay pairs never straddle ranks."""
     assert n % 2 == 0, "envs per GPU must be even (selfplay pairs)"
-    return rank * n, (rank + 1) * n
+    assert nsp == 0 or nbot == 0, "a shard is all selfplay or all bot envs"
+    return rank * n, rank * (nsp // 2 + nbot)
 
 
 def kernel_bytes(G, N, HW, P=29, eager=True, sampler="src", src_rows=0):
@@ -191,27 +269,26 @@ def run_gpu(args, rank, world, local_rank):
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     n = args.envs_per_gpu
-    shard(rank, n)
     from gym_microrts import microrts_ai
 
     wmap, nsp, nbot, bot, po = WORKLOADS[args.workload]
     nsp = n if nsp == "all" else nsp
     nbot = n if nbot == "all" else nbot
+    env0, game_offset = shard(rank, n, nsp, nbot)
     if args.api == "sharedmem":
         from gym_microrts.envs.vec_env import MicroRTSGridModeSharedMemVecEnv as Env
         extra = {}
     else:
         Env = MicroRTSGridModeVecEnv
         extra = dict(return_tensors=args.api == "tensor", eager_masks=not args.no_eager_masks,
-                     bot_fusion=args.bot_fusion)
+                     bot_fusion=args.bot_fusion, game_offset=game_offset)
     env = Env(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=args.max_steps, map_paths=[wmap],
               ai2s=[getattr(microrts_ai, bot)] * nbot if nbot else [], partial_obs=po,
               reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, **extra)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
     lib = _native.lib()
-    # shard-specific seed: rank r's envs are global envs [r*n, (r+1)*n)
-    seed = (args.seed << 32) | rank
+    seed = args.seed   # one stream over global env indices: rank r samples envs [env0, env0 + n)
     ev = {}
 
     def one_step(s):
@@ -223,7 +300,7 @@ def run_gpu(args, rank, world, local_rank):
         if env.kernel_events is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        rc = sample(lib, args.sampler, env._mask, env._src, n, hw, seed, s, act)
+        rc = sample(lib, args.sampler, env._mask, env._src, n, hw, env0, seed, s, act)
         if env.kernel_events is not None:
             e1.record()
             env.kernel_events.setdefault("sample", []).append((e0, e1))
@@ -234,24 +311,40 @@ def run_gpu(args, rank, world, local_rank):
 
     timing = [False]
     env.reset()
-    for s in range(args.warmup):
+    s0 = preroll([env], one_step, args.max_steps if args.preroll < 0 else args.preroll, rank, world)
+    for s in range(s0, s0 + args.warmup):
         one_step(s)
+    torch.cuda.synchronize()
+    before = [env.game_stats()]
     timing[0] = not args.no_kernel_events
     barrier(world, dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.warmup, args.warmup + args.steps):
+    for s in range(s0 + args.warmup, s0 + args.warmup + args.steps):
         obs, rew, done, infos = one_step(s)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world, dev)
     elapsed = t1 - t0
     env.kernel_events = None
+    stats = window_stats(before, [env.game_stats()], args.steps)
+    stats["preroll_ticks"] = s0
+    if args.dump:
+        np.savez(f"{args.dump}.rank{rank}.npz", obs=obs.cpu().numpy(), mask=env._mask.cpu().numpy(),
+                 src=env._src.cpu().numpy(), raw=env._raw.cpu().numpy(), done=env._done.cpu().numpy(),
+                 stats=env.game_stats(), env0=env0)
     flags = env.error_flags()
     kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
     G = nsp // 2 + nbot
     src_rows = int(env._src.sum().item())   # source cells of the last step (sampler bytes)
-    return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes), src_rows
+    return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes), src_rows, stats
+
+
+def _coll_device(dev):
+    """collectives run on the GPU under RCCL, on the host under gloo"""
+    import torch.distributed as dist
+
+    return dev if dist.get_backend() == "nccl" else "cpu"
 
 
 def barrier(world, dev):
@@ -259,7 +352,7 @@ def barrier(world, dev):
         import torch
         import torch.distributed as dist
 
-        t = torch.ones(1, device=dev)
+        t = torch.ones(1, device=_coll_device(dev))
         dist.all_reduce(t)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
@@ -271,7 +364,7 @@ def max_over_ranks(x, world, dev):
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device(dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -323,6 +416,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    # one GPU per rank; ranks beyond the visible GPUs share them (gloo shard tests on a 1-GPU box)
+    local_rank %= max(1, torch.cuda.device_count())
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     import torch
@@ -331,12 +428,15 @@ def main():
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
     if args.workload == "mixed":
         torch.cuda.set_device(local_rank)
-        elapsed, kern, flags, hw, G, N, P, src_rows = run_mixed(args, rank, torch.device("cuda", local_rank))
+        elapsed, kern, flags, hw, G, N, P, src_rows, stats = run_mixed(args, rank, torch.device("cuda", local_rank))
     else:
-        elapsed, kern, flags, hw, G, N, P, src_rows = run_gpu(args, rank, world, local_rank)
+        elapsed, kern, flags, hw, G, N, P, src_rows, stats = run_gpu(args, rank, world, local_rank)
     dev = torch.device("cuda", local_rank)
     elapsed_max = max_over_ranks(elapsed, world, dev)
     total_env_steps = world * N * args.steps
@@ -356,12 +456,23 @@ def main():
         dom = max((k for k in kern if k in kb), key=lambda k: kern[k], default=None)
         if dom:
             achieved = kb[dom] / (kern[dom] * 1e-3) / 1e9
-            traffic, tsrc = pmc_traffic(dom)
+            # the committed PMC summary is of the headline command (selfplay, 8192 envs) only
+            headline = args.workload == "selfplay" and N == 8192 and args.api == "tensor"
+            traffic, tsrc = pmc_traffic(dom) if headline else (None, None)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else round(traffic / (kern[dom] * 1e-3) / 1e9, 1),
                     "traffic_bytes_per_launch": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": kb[dom], "kernel": dom, "avg_launch_ms": round(kern[dom], 4)}
+        bk = stats.get("buckets")
+        if bk and all(b["step_ms"] for b in bk):
+            # configs[4]: one step kernel per size bucket, back to back -- the algorithmic
+            # bytes of all buckets over the sum of their mean launch times
+            tb, tms = sum(b["step_bytes"] for b in bk), sum(b["step_ms"] for b in bk)
+            achieved = tb / (tms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": tb,
+                    "kernel": "step (sum over the size buckets)", "avg_launch_ms": round(tms, 4)}
         env_step_bytes = hw * (4 * P + 312 + 56 + 32) + 64   # SURVEY.md §8d whole-step formula
         out = {
             "metric": METRIC,
@@ -387,6 +498,7 @@ def main():
             "env_step_bytes": env_step_bytes,
             "env_step_roofline_frac": round(value / world * env_step_bytes / (HBM_PEAK_GBS * 1e9), 4),
             "engine_error_flags": flags,
+            "window": stats,
         }
         if args.workload != "selfplay":
             out["metric"] = f"env-steps/sec, workload {args.workload} (secondary config, not the BASELINE metric)"

@@ -71,6 +71,11 @@ typedef struct {
     const int32_t *bot_ai0;      /* [num_bot_envs] MRTS_AI_* of player 0 (bot vs bot,
                                     MicroRTSBotVecEnv / JNIBotClient, vec_env.py:1104-1236),
                                     -1 = the agent plays player 0; NULL = all agent */
+    int32_t game_offset;         /* global index of game 0 when this handle is one shard
+                                    of a larger batch (one process per GPU): keys the
+                                    random bots' streams so shard r's games play exactly
+                                    as games [game_offset, game_offset + num_games) of
+                                    one unsharded run; 0 otherwise                    */
 } mrts_config;
 
 typedef struct {
@@ -151,15 +156,27 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);
 
 /* Random masked action sampler of hello_world.py:27-64 on the device
- * (Philox4x32-10 keyed by seed, counter = (cell, env, step)). */
-int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int32_t hw, uint64_t seed,
+ * (Philox4x32-10 keyed by seed, counter = (cell, env0 + env, step)): env0 is the
+ * global index of row 0's env, so a shard draws the actions of its slice of
+ * one larger batch.  Not a reference entry point: the bench's stand-in policy. */
+int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int32_t hw, int32_t env0, uint64_t seed,
                         uint32_t step, int64_t *actions);
 
 /* Same stream and output as mrts_sample_actions, given the source channel too:
  * mask rows of cells whose source is 0 are all zero (getMasks), so only the
  * rows of source cells are read.  Every row's 7 components are still written. */
 int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t num_envs, int32_t hw,
-                            uint64_t seed, uint32_t step, int64_t *actions);
+                            int32_t env0, uint64_t seed, uint32_t step, int64_t *actions);
+
+/* Per-game rollout statistics, host int32 out[num_games][MRTS_GAME_STATS]:
+ * game time (ticks since the game's last reset; the reference's gs.getTime()),
+ * env steps of the episode, steps since creation, and three never-reset
+ * counters -- ticks whose ready actions executed in order on one lane (attacks
+ * or a shared resource pile), action rows issued on the ordered one-lane path,
+ * auto-resets.  Synchronises the stream.  Introspection only (bench.py reports
+ * the episode phases and serial work its timed window covered). */
+#define MRTS_GAME_STATS 6
+int mrts_game_stats(mrts_vec *h, void *stream, int32_t *out);
 
 /* render("rgb_array") (vec_env.py:1075-1084): the game of `env` drawn into a
  * device frame rgb [size][size][3] uint8 (RGB; the reference returns 640 x 640).

@@ -821,7 +821,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     S.HW = HW;
     S.player = player;
     S.partial = p.partial_obs;
-    S.game = g;
+    S.game = p.game_offset + g;
     S.tick = (uint32_t)genv[MRTS_G_TICKS];
     S.res[0] = genv[MRTS_G_RES0];
     S.res[1] = genv[MRTS_G_RES1];

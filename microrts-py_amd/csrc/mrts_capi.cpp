@@ -158,6 +158,7 @@ struct mrts_vec {
     std::vector<int32_t> bot_ai;
     std::vector<int32_t> bot_ai0;   // -1: the agent plays player 0
     int nbot0 = 0;
+    int game_offset = 0;
     // workspace carving
     size_t off_cells = 0, off_genv = 0, off_mcells = 0, off_mwall = 0, off_mscal = 0, off_scratch = 0, total = 0;
     size_t off_botai = 0, off_botai0 = 0, off_aa = 0, off_botpa = 0;
@@ -231,6 +232,8 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
         h->bot_ai[j] = a;
         h->nbot_active += a != MRTS_AI_PASSIVE;
     }
+    if (cfg->game_offset < 0) return fail(h, MRTS_EINVAL, "game_offset must be >= 0");
+    h->game_offset = cfg->game_offset;
     h->bot_ai0.assign(h->nbot, -1);
     h->nbot0 = 0;
     for (int j = 0; cfg->bot_ai0 && j < h->nbot; j++) {
@@ -324,6 +327,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.aa = h->nbot_active ? (int4 *)(h->ws + h->off_aa) : nullptr;
     p.botpa = h->nbot_active ? (int32_t *)(h->ws + h->off_botpa) : nullptr;
     p.nbot_active = h->nbot_active;
+    p.game_offset = h->game_offset;
     h->err.clear();
     return MRTS_OK;
 }
@@ -468,16 +472,16 @@ int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int3
     return e ? hip_fail(h, e, "reset_games sync") : MRTS_OK;
 }
 
-int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw, uint64_t seed, uint32_t step,
+int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw, int32_t env0, uint64_t seed, uint32_t step,
                         int64_t *actions) {
-    if (!mask || !actions || n < 0 || hw <= 0) return MRTS_EINVAL;
-    return mrts_engine_sample(mask, n, hw, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
+    if (!mask || !actions || n < 0 || hw <= 0 || env0 < 0) return MRTS_EINVAL;
+    return mrts_engine_sample(mask, n, hw, env0, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
 }
 
-int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t n, int32_t hw, uint64_t seed,
-                            uint32_t step, int64_t *actions) {
-    if (!mask || !source || !actions || n < 0 || hw <= 0) return MRTS_EINVAL;
-    return mrts_engine_sample_src(mask, source, n, hw, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
+int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t n, int32_t hw, int32_t env0,
+                            uint64_t seed, uint32_t step, int64_t *actions) {
+    if (!mask || !source || !actions || n < 0 || hw <= 0 || env0 < 0) return MRTS_EINVAL;
+    return mrts_engine_sample_src(mask, source, n, hw, env0, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
 }
 
 int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source) {
@@ -496,6 +500,19 @@ int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t si
     const int game = env < h->nsp ? env / 2 : h->nsp / 2 + (env - h->nsp);
     hipError_t e = mrts_engine_render(&h->base, (hipStream_t)stream, game, h->game_map[game], size, rgb);
     return e ? hip_fail(h, e, "render launch") : MRTS_OK;
+}
+
+int mrts_game_stats(mrts_vec *h, void *stream, int32_t *out) {
+    if (!bound(h) || !out) return fail(h, MRTS_ESTATE, "game_stats: not bound or out null");
+    std::vector<int32_t> genv((size_t)h->ngames * MRTS_GENV_WORDS);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemcpyAsync(genv.data(), h->ws + h->off_genv, genv.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (!e) e = hipStreamSynchronize(s);
+    if (e) return hip_fail(h, e, "game_stats readback");
+    static const int words[MRTS_GAME_STATS] = {MRTS_G_TIME, MRTS_G_STEPS, MRTS_G_TICKS, MRTS_G_SERIAL, MRTS_G_ORDERED, MRTS_G_EPISODES};
+    for (int g = 0; g < h->ngames; g++)
+        for (int k = 0; k < MRTS_GAME_STATS; k++) out[(size_t)g * MRTS_GAME_STATS + k] = genv[(size_t)g * MRTS_GENV_WORDS + words[k]];
+    return MRTS_OK;
 }
 
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {

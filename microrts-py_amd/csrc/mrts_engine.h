@@ -35,6 +35,7 @@ struct EngineParams {
     const int32_t *bot_games; // k_bot: decide only for these games (device list), null = every bot game
     int bot_ngames;
     int fuse_bots;          // k_step: wave 0 of each bot game's workgroup decides the next tick's bot actions
+    int game_offset;        // global index of game 0 (a shard of a larger batch): keys the bots' RNG
 };
 
 extern "C" {
@@ -43,9 +44,9 @@ hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_bots(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *raw);
-hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
-hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n, int hw, uint64_t seed, uint32_t step, int64_t *act,
-                                  hipStream_t s);
+hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
+hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n, int hw, int env0, uint64_t seed, uint32_t step,
+                                  int64_t *act, hipStream_t s);
 hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, int map, int size, uint8_t *rgb);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);

@@ -340,7 +340,12 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
     Lds L = carve(smem, p.HW, p.W, NT);
     int g = games ? games[blockIdx.x] : blockIdx.x;
     int map = maps ? maps[blockIdx.x] : p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
-    if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = threadIdx.x == SC_TICKS ? p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_TICKS] : 0;
+    // a reset keeps the never-reset counters (bot RNG ticks, rollout statistics)
+    if (threadIdx.x < SC_WORDS) {
+        const int w = threadIdx.x;
+        const bool keep = w == SC_TICKS || w == MRTS_G_SERIAL || w == MRTS_G_ORDERED || w == MRTS_G_EPISODES;
+        L.sc[w] = keep ? p.genv[(size_t)g * MRTS_GENV_WORDS + w] : 0;
+    }
     __syncthreads();
     reset_into_lds<NT>(p, L, map);
     __syncthreads();
@@ -881,6 +886,8 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     if (threadIdx.x == 0) {
         L.sc[SC_TIME] = now;
         L.sc[SC_TICKS]++;
+        L.sc[MRTS_G_SERIAL] += serial;      // rollout statistics (mrts_game_stats)
+        L.sc[MRTS_G_ORDERED] += nrows;
         if (now >= MRTS_MAX_TIME) L.sc[SC_ERR] |= MRTS_ERR_TIME_OVERFLOW;
         if (!serial)
             for (int i = 0; i < nready; i++) L.sc[SC_UID] += code_type(L.snap[i].z) == A_PRODUCE;
@@ -920,7 +927,10 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     __syncthreads();
     if (reset) {
         reset_into_lds<NT>(p, L, L.sc[SC_MAP]);
-        if (threadIdx.x == 0) L.sc[SC_AA_N] = L.sc[MRTS_G_AA_N0] = 0;   // ai1 / ai2.reset()
+        if (threadIdx.x == 0) {
+            L.sc[SC_AA_N] = L.sc[MRTS_G_AA_N0] = 0;   // ai1 / ai2.reset()
+            L.sc[MRTS_G_EPISODES]++;
+        }
         __syncthreads();
     } else if (threadIdx.x == 0) {
         L.sc[SC_STEPS] = steps;
@@ -998,7 +1008,9 @@ __global__ __launch_bounds__(256) void k_render(const int4* __restrict__ cells, 
 // ---------------------------------------------------------------------------
 // Counter-based masked sampler (hello_world.py:27-64 semantics), Philox4x32-10
 // keyed (seed) with counter (cell, env, step, half) -- identical stream to the
-// oracle's ovec_sample_actions.  One lane per (env, cell).
+// oracle's ovec_sample_actions.  `env` is the GLOBAL env index (env0 + local
+// row), so a shard of envs [env0, env0 + n) draws exactly the actions of that
+// slice of one larger run (multi-GPU sharding).
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
@@ -1076,7 +1088,7 @@ __device__ __forceinline__ void sample_load(SampleBuf& B, const int32_t* __restr
 }
 
 __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* __restrict__ mask, long long grp, long long rows,
-                                             int hw, uint64_t seed, uint32_t step, int64_t* __restrict__ act,
+                                             int hw, int env0, uint64_t seed, uint32_t step, int64_t* __restrict__ act,
                                              uint32_t* s_bits, int64_t* s_out) {
     const int lane = threadIdx.x & 63;
     const long long row0 = grp * SW;
@@ -1110,7 +1122,7 @@ __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* 
         const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
         const uint64_t lo = (uint64_t)s_bits[3 * lane] | ((uint64_t)s_bits[3 * lane + 1] << 32);
         const uint64_t hi = s_bits[3 * lane + 2];
-        sample_row(lo, hi, e, c, seed, step, s_out + lane * 7);
+        sample_row(lo, hi, env0 + e, c, seed, step, s_out + lane * 7);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int64_t* ob = act + row0 * 7;   // 16-B aligned: SW * 56 B per group
@@ -1123,8 +1135,8 @@ __device__ __forceinline__ void sample_group(const SampleBuf& B, const int32_t* 
 }
 
 constexpr int SAMPLE_BLOCKS_PER_CU = 16;   // measured best (round 1: 2 -> 151 us, 4 -> 138, 8 -> 133, 16 -> 127, 64 -> 178)
-__global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, uint64_t seed,
-                                                        uint32_t step, int64_t* __restrict__ act) {
+__global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restrict__ mask, int n, int hw, int env0,
+                                                        uint64_t seed, uint32_t step, int64_t* __restrict__ act) {
     __shared__ uint32_t s_bits[SWAVES][SW * 3];
     __shared__ __attribute__((aligned(16))) int64_t s_out[SWAVES][SW * 7];
     const int w = threadIdx.x >> 6;
@@ -1138,11 +1150,11 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restric
     while (true) {   // two groups per trip: A is consumed while B loads, then the reverse
         const long long g1 = grp + stride;   // past the end: a harmless re-read of the last group
         sample_load(B, mask, min(g1, ngrp - 1), rows);
-        sample_group(A, mask, grp, rows, hw, seed, step, act, s_bits[w], s_out[w]);
+        sample_group(A, mask, grp, rows, hw, env0, seed, step, act, s_bits[w], s_out[w]);
         if (g1 >= ngrp) break;
         const long long g2 = g1 + stride;
         sample_load(A, mask, min(g2, ngrp - 1), rows);
-        sample_group(B, mask, g1, rows, hw, seed, step, act, s_bits[w], s_out[w]);
+        sample_group(B, mask, g1, rows, hw, env0, seed, step, act, s_bits[w], s_out[w]);
         if (g2 >= ngrp) break;
         grp = g2;
     }
@@ -1158,7 +1170,8 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restric
 // up to four rows in flight) and folds each with two ballots.
 constexpr int SR_WAVES = 4;
 __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n,
-                                                           int hw, uint64_t seed, uint32_t step, int64_t* __restrict__ act) {
+                                                           int hw, int env0, uint64_t seed, uint32_t step,
+                                                           int64_t* __restrict__ act) {
     __shared__ __attribute__((aligned(16))) int64_t s_out[SR_WAVES][64 * 7];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long rows = (long long)n * hw;
@@ -1193,7 +1206,7 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
     if (in) {
         const long long idx = row0 + lane;
         const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
-        sample_row(lo, hi, e, c, seed, step, s_out[w] + lane * 7);
+        sample_row(lo, hi, env0 + e, c, seed, step, s_out[w] + lane * 7);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int64_t* ob = act + row0 * 7;   // 16-B aligned: 64 * 56 B per wave
@@ -1276,21 +1289,21 @@ hipError_t mrts_engine_raw_obs(const EngineParams* p, hipStream_t s, int32_t* ra
     return hipGetLastError();
 }
 hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 2, s, nullptr, nullptr, 0); }
-hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
+hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
     int total = n * hw;
     if (total == 0) return hipSuccess;
     // persistent grid: enough waves to keep every CU streaming, each looping over row groups
     const long long groups = ((long long)total + mrts::SW - 1) / mrts::SW;
     const long long blocks = std::min<long long>((groups + mrts::SWAVES - 1) / mrts::SWAVES, 256 * mrts::SAMPLE_BLOCKS_PER_CU);   // resident blocks
-    hipLaunchKernelGGL(mrts::k_sample, dim3((unsigned)blocks), dim3(64 * mrts::SWAVES), 0, s, mask, n, hw, seed, step, act);
+    hipLaunchKernelGGL(mrts::k_sample, dim3((unsigned)blocks), dim3(64 * mrts::SWAVES), 0, s, mask, n, hw, env0, seed, step, act);
     return hipGetLastError();
 }
-hipError_t mrts_engine_sample_src(const int32_t* mask, const int32_t* src, int n, int hw, uint64_t seed, uint32_t step, int64_t* act,
-                                  hipStream_t s) {
+hipError_t mrts_engine_sample_src(const int32_t* mask, const int32_t* src, int n, int hw, int env0, uint64_t seed, uint32_t step,
+                                  int64_t* act, hipStream_t s) {
     const long long rows = (long long)n * hw;
     if (rows == 0) return hipSuccess;
     const long long blocks = (rows + 64 * mrts::SR_WAVES - 1) / (64 * mrts::SR_WAVES);
-    hipLaunchKernelGGL(mrts::k_sample_src, dim3((unsigned)blocks), dim3(64 * mrts::SR_WAVES), 0, s, mask, src, n, hw, seed, step, act);
+    hipLaunchKernelGGL(mrts::k_sample_src, dim3((unsigned)blocks), dim3(64 * mrts::SR_WAVES), 0, s, mask, src, n, hw, env0, seed, step, act);
     return hipGetLastError();
 }
 hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, int map, int size, uint8_t* rgb) {

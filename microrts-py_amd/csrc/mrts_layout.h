@@ -32,9 +32,14 @@
 /* per-game scalars; AA_N..NPA are used by bot games only:
  *   AA_N  entries of the bot's AbstractionLayerAI.actions list (mrts_bots.hip)
  *   TICKS steps since creation (never reset; bot RNG counter)
- *   NPA   entries of the bot PlayerAction handed from k_bot to k_step */
+ *   NPA   entries of the bot PlayerAction handed from k_bot to k_step
+ * rollout statistics, never reset (mrts_game_stats):
+ *   SERIAL   ticks whose ready set executed in order on one lane (attacks, shared piles)
+ *   ORDERED  action rows issued on the ordered (one-lane) path
+ *   EPISODES auto-resets (gameover or max_steps) */
 enum { MRTS_G_TIME = 0, MRTS_G_RES0, MRTS_G_RES1, MRTS_G_NEXT_UID, MRTS_G_STEPS, MRTS_G_MAP, MRTS_G_ERR, MRTS_G_AA_N,
-       MRTS_G_TICKS, MRTS_G_NPA, MRTS_G_AA_N0, MRTS_G_NPA0, MRTS_GENV_WORDS = 16 };   /* *0: player-0 bot (bot vs bot) */
+       MRTS_G_TICKS, MRTS_G_NPA, MRTS_G_AA_N0, MRTS_G_NPA0, MRTS_G_SERIAL, MRTS_G_ORDERED, MRTS_G_EPISODES,
+       MRTS_GENV_WORDS = 16 };   /* *0: player-0 bot (bot vs bot) */
 enum { MRTS_M_RES0 = 0, MRTS_M_RES1, MRTS_M_NUNITS, MRTS_M_PAD, MRTS_MAP_SCALARS };
 
 /* error bits recorded in genv[MRTS_G_ERR] (invariant violations) */

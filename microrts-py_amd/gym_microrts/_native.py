@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmicrorts
 MRTS_OK = 0
 MRTS_OBS_INT32 = 0
 MRTS_OBS_FLOAT32 = 1
+MRTS_GAME_STATS = 6
 ERROR_NAMES = {-1: "EINVAL", -2: "EIO", -3: "EHIP", -4: "ENOTIMPL", -5: "ESTATE"}
 
 
@@ -45,6 +46,7 @@ class Config(ctypes.Structure):
         ("bot_ai", ctypes.POINTER(ctypes.c_int32)),
         ("obs_dtype", ctypes.c_int32),
         ("bot_ai0", ctypes.POINTER(ctypes.c_int32)),
+        ("game_offset", ctypes.c_int32),
     ]
 
 
@@ -74,8 +76,10 @@ SIGNATURES = {
     "mrts_set_reward_weight": (ctypes.c_int, [P, P, ctypes.c_int32]),
     "mrts_step_weighted": (ctypes.c_int, [P, P, P, P, P, P, P, P, P]),
     "mrts_reset_games": (ctypes.c_int, [P, P, P, P, ctypes.c_int32, P]),
-    "mrts_sample_actions": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
-    "mrts_sample_actions_src": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
+    "mrts_sample_actions": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
+    "mrts_sample_actions_src": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                               ctypes.c_uint32, P]),
+    "mrts_game_stats": (ctypes.c_int, [P, P, P]),
     "mrts_bind_mask_outputs": (ctypes.c_int, [P, P, P]),
     "mrts_set_bot_fusion": (ctypes.c_int, [P, ctypes.c_int32]),
     "mrts_render": (ctypes.c_int, [P, P, ctypes.c_int32, P, ctypes.c_int32]),
@@ -113,7 +117,8 @@ def check(rc, handle=None, what="call"):
         raise cls(f"libmicrorts_amd {what} failed ({ERROR_NAMES.get(rc, rc)}): {msg}")
 
 
-def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, game_map, bot_ai, obs_dtype, bot_ai0=None):
+def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, game_map, bot_ai, obs_dtype, bot_ai0=None,
+           game_offset=0):
     cfg = Config()
     cfg.num_selfplay_envs = num_selfplay_envs
     cfg.num_bot_envs = num_bot_envs
@@ -127,6 +132,7 @@ def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, g
     cfg.game_map = ctypes.cast(gm, ctypes.POINTER(ctypes.c_int32))
     cfg.bot_ai = ctypes.cast(ai, ctypes.POINTER(ctypes.c_int32))
     cfg.obs_dtype = obs_dtype
+    cfg.game_offset = int(game_offset)
     if bot_ai0 is not None:
         a0 = (ctypes.c_int32 * max(1, len(bot_ai0)))(*bot_ai0)
         cfg.bot_ai0 = ctypes.cast(a0, ctypes.POINTER(ctypes.c_int32))

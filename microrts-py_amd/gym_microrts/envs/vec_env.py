@@ -129,6 +129,7 @@ class MicroRTSGridModeVecEnv:
         obs_dtype=None,
         eager_masks=True,
         bot_fusion=True,
+        game_offset=0,
         _ai1s=None,
     ):
         # vec_env.py:110-127
@@ -203,7 +204,7 @@ class MicroRTSGridModeVecEnv:
         # new JNIGridnetVecClient(...) (vec_env.py:256-276)
         self._h = _native.create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, self._map_table, game_map,
                                  bot_ai, _native.MRTS_OBS_FLOAT32 if obs_dtype == torch.float32 else _native.MRTS_OBS_INT32,
-                                 bot_ai0=bot_ai0)
+                                 bot_ai0=bot_ai0, game_offset=game_offset)
         self._game_map = list(game_map)
         info = _native.info(self._h)
         assert (info.height, info.width) == (self.height, self.width)
@@ -361,30 +362,49 @@ class MicroRTSGridModeVecEnv:
         infos = [{"raw_rewards": item} for item in reward]
         return obs, reward @ self.reward_weight, done[:, 0], infos
 
+    def game_of_env(self, e):
+        """env index -> game index (selfplay pairs 2k / 2k+1 share game k, then bot envs)."""
+        nsp = self.num_selfplay_envs
+        return e // 2 if e < nsp else nsp // 2 + (e - nsp)
+
+    def reset_games(self, games, maps=None):
+        """Reset the given games (their envs' obs, and masks when eager) onto `maps`
+        (map-table indices; default: each game's current map) -- the per-client
+        reset of the reference's map cycling (vec_env.py:1044-1054)."""
+        import ctypes
+
+        games = [int(g) for g in games]
+        if not games:
+            return
+        maps = [self._game_map[g] for g in games] if maps is None else [int(m) for m in maps]
+        for g, m in zip(games, maps):
+            self._game_map[g] = m
+        ga = (ctypes.c_int32 * len(games))(*games)
+        ma = (ctypes.c_int32 * len(maps))(*maps)
+        _native.check(_native.lib().mrts_reset_games(self._h, self._stream(), ga, ma, len(games), self._obs.data_ptr()), self._h,
+                      "reset_games")
+
+    def game_stats(self):
+        """(num_games, 6) int32: game time, episode env steps, steps since creation, serial
+        ticks, ordered-path rows, auto-resets (mrts_game_stats)."""
+        out = np.zeros((self._n_games(), _native.MRTS_GAME_STATS), np.int32)
+        _native.check(_native.lib().mrts_game_stats(self._h, self._stream(), out.ctypes.data), self._h, "game_stats")
+        return out
+
+    def _n_games(self):
+        return self.num_selfplay_envs // 2 + self.num_bot_envs
+
     def _cycle(self, done0):
         """vec_env.py:1038-1056 map cycling, indexed the engine's way (selfplay
         pairs first, then bot envs)."""
         games, maps = [], []
         nsp = self.num_selfplay_envs
         for e in np.nonzero(done0)[0]:
-            if e < nsp:
-                if e % 2:
-                    continue
-                g = e // 2
-            else:
-                g = nsp // 2 + (e - nsp)
-            m = self._map_index[next(self.next_map)]
-            games.append(g)
-            maps.append(m)
-            self._game_map[g] = m
-        if games:
-            import ctypes
-
-            ga = (ctypes.c_int32 * len(games))(*games)
-            ma = (ctypes.c_int32 * len(maps))(*maps)
-            _native.check(
-                _native.lib().mrts_reset_games(self._h, self._stream(), ga, ma, len(games), self._obs.data_ptr()), self._h, "reset_games"
-            )
+            if e < nsp and e % 2:
+                continue
+            games.append(self.game_of_env(e))
+            maps.append(self._map_index[next(self.next_map)])
+        self.reset_games(games, maps)
 
     def step(self, ac):
         self.step_async(ac)

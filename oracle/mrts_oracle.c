@@ -986,11 +986,11 @@ static void sample_row(const int32_t *m, int e, int c, uint64_t seed, uint32_t s
     }
 }
 
-void ovec_sample_actions(const int32_t *m78, int n, int hw, uint64_t seed, uint32_t step, int64_t *act) {
+void ovec_sample_actions(const int32_t *m78, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t *act) {
 #pragma omp parallel for schedule(static)
     for (int e = 0; e < n; e++)
         for (int c = 0; c < hw; c++)
-            sample_row(m78 + ((size_t)e * hw + c) * 78, e, c, seed, step, act + ((size_t)e * hw + c) * 7);
+            sample_row(m78 + ((size_t)e * hw + c) * 78, env0 + e, c, seed, step, act + ((size_t)e * hw + c) * 7);
 }
 
 /* The bench's CPU baseline: `steps` env-steps of every env -- getMasks, the

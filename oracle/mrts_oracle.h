@@ -84,8 +84,8 @@ void ovec_dump_cells(const OVec *v, int game, int32_t *out);
  * sampler (hello_world.py:27-64 semantics: per cell and component, uniform
  * over mask-valid entries; uniform over all entries when none is valid).
  * masks: [N][H*W][78] (channels 1..78 of getMasks), actions out [N][H*W][7]. */
-void ovec_sample_actions(const int32_t *masks78, int n, int hw, uint64_t seed,
-                         uint32_t step, int64_t *actions);
+void ovec_sample_actions(const int32_t *masks78, int n, int hw, int env0, uint64_t seed,
+                         uint32_t step, int64_t *actions);   /* env0: global index of row 0's env */
 
 /* CPU baseline of bench.py: `steps` whole env-steps (masks, sampler, step,
  * obs encode) with OpenMP over envs; see mrts_oracle.c. */

@@ -48,7 +48,7 @@ def lib():
         L.ovec_game_time.restype = ctypes.c_int
         L.ovec_game_resources.argtypes = [P, ctypes.c_int, P]
         L.ovec_dump_cells.argtypes = [P, ctypes.c_int, P]
-        L.ovec_sample_actions.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P]
+        L.ovec_sample_actions.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P]
         L.ovec_bench_steps.argtypes = [P, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P, P, P, P, P, P]
         _lib = L
     return _lib
@@ -195,12 +195,13 @@ class OracleVecEnv:
         return out
 
 
-def sample_actions(masks78, seed, step):
-    """Philox-keyed masked sampler (same stream as the GPU bench sampler)."""
+def sample_actions(masks78, seed, step, env0=0):
+    """Philox-keyed masked sampler (same stream as the GPU bench sampler); env0 =
+    global index of row 0's env (a shard of a larger batch)."""
     m = np.ascontiguousarray(masks78, dtype=np.int32)
     n, hw = m.shape[0], m.shape[1]
     out = np.zeros((n, hw, 7), np.int64)
-    lib().ovec_sample_actions(ptr(m), n, hw, ctypes.c_uint64(seed), ctypes.c_uint32(step), ptr(out))
+    lib().ovec_sample_actions(ptr(m), n, hw, env0, ctypes.c_uint64(seed), ctypes.c_uint32(step), ptr(out))
     return out
 
 

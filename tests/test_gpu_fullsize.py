@@ -81,3 +81,56 @@ def test_fullsize_partial_obs_4096():
 def test_fullsize_24x24_4096():
     """configs[4]'s largest bucket map at 4096 envs, with workerRush bot envs."""
     _full_rollout("maps/24x24/basesWorkers24x24.xml", 2048, 2048, "workerRushAI", steps=100, max_steps=80)
+
+
+@pytest.mark.timeout(1000)
+def test_fullsize_2000_tick_episode_1024():
+    """A whole 2000-tick episode (max_steps 2000) at 1024 envs vs the
+    oracle, through the bench's staggered pre-roll: games 0..255 run from reset to
+    the time-limit reset at tick 2000, games 256..511 are reset at staggered ticks
+    (bench.stagger_plan) so every phase of an episode -- mid-game fights, gameovers,
+    auto-resets at every tick -- is stepped too.  Rewards / dones every step, the
+    whole obs / mask / source tensors every 10th step and at the end."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv, sample_actions
+
+    m = "maps/16x16/basesWorkers16x16.xml"
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=1024, num_bot_envs=0, max_steps=2000, map_paths=[m], reward_weight=W,
+                               return_tensors=True, obs_dtype=torch.int32)
+    o = OracleVecEnv(1024, 0, [os.path.join(MAPS, m)], max_steps=2000, reward_weight=W)
+    dev = g.device
+
+    def same(gpu, host, what, s):
+        assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"{what} differs at step {s}"
+
+    same(g.reset(), o.reset(), "reset obs", -1)
+    plan = bench.stagger_plan(256, 1000)
+    ends = 0
+    for s in range(2100):
+        mo = o.get_action_mask()
+        a = sample_actions(mo, 31, s)
+        og, rg, dg, ig = g.step(torch.from_numpy(a).to(dev))
+        oo, ro, do, io = o.step(a)
+        same(ig._raw, np.array([i["raw_rewards"] for i in io]), "raw rewards", s)
+        same(dg, np.asarray(do, bool), "done", s)
+        ends += int(np.asarray(do).sum())
+        if s < 1000 and plan[s]:
+            games = [256 + k for k in plan[s]]
+            g.reset_games(games)
+            for k in games:
+                o.reset_game(k, 0)
+            oo = o.encode(o.raw_obs())
+        if s % 10 == 0 or s == 2099:
+            same(og, oo, "obs", s)
+            same(g.get_action_mask(), o.get_action_mask(), "mask", s)
+            same(g.source_unit_mask, o.source_unit_mask, "source", s)
+    st = g.game_stats()
+    assert (st[:256, 5] >= 1).all()            # every unstaggered game finished an episode
+    assert ends >= 512                         # games 0..255 (both views) reset at tick 2000
+    assert g.error_flags() == 0

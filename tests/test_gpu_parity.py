@@ -186,7 +186,7 @@ def test_eager_masks_equal_mask_kernel(map_path):
         _native.check(_native.lib().mrts_get_masks(g._h, st, m2.data_ptr(), s2.data_ptr()), g._h, "get_masks")
         assert torch.equal(m, m2), f"mask step {s}"
         assert torch.equal(g.source_unit_mask, s2), f"source step {s}"
-        _native.check(_native.lib().mrts_sample_actions(st, m.data_ptr(), g.num_envs, hw, ctypes.c_uint64(5), s, act.data_ptr()))
+        _native.check(_native.lib().mrts_sample_actions(st, m.data_ptr(), g.num_envs, hw, 0, ctypes.c_uint64(5), s, act.data_ptr()))
         g.step(act)
     assert g.error_flags() == 0
 
@@ -208,8 +208,8 @@ def test_source_guided_sampler_equals_dense_sampler():
     for s in range(60):
         m = g.get_action_mask()
         seed = ctypes.c_uint64(0x0123456789ABCDEF + s)
-        _native.check(_native.lib().mrts_sample_actions(st, m.data_ptr(), 256, 256, seed, s, a1.data_ptr()))
-        _native.check(_native.lib().mrts_sample_actions_src(st, m.data_ptr(), g.source_unit_mask.data_ptr(), 256, 256, seed, s,
+        _native.check(_native.lib().mrts_sample_actions(st, m.data_ptr(), 256, 256, 0, seed, s, a1.data_ptr()))
+        _native.check(_native.lib().mrts_sample_actions_src(st, m.data_ptr(), g.source_unit_mask.data_ptr(), 256, 256, 0, seed, s,
                                                             a2.data_ptr()))
         assert torch.equal(a1, a2), f"step {s}"
         if s % 20 == 0:
@@ -235,7 +235,7 @@ def test_source_guided_sampler_ragged_rows(rows):
     md, sd = torch.from_numpy(m).cuda(), torch.from_numpy(src).cuda()
     out = torch.full((1, rows, 7), -1, dtype=torch.int64, device="cuda")
     _native.check(_native.lib().mrts_sample_actions_src(torch.cuda.current_stream().cuda_stream, md.data_ptr(), sd.data_ptr(), 1,
-                                                        rows, ctypes.c_uint64(42), 7, out.data_ptr()))
+                                                        rows, 0, ctypes.c_uint64(42), 7, out.data_ptr()))
     np.testing.assert_array_equal(out.cpu().numpy(), sample_actions(m, 42, 7))
 
 
@@ -259,7 +259,7 @@ def test_device_sampler_matches_oracle_sampler():
     m = g.get_action_mask()
     out = torch.empty((64, 256, 7), dtype=torch.int64, device=g.device)
     for step in (0, 1, 12345):
-        _native.check(_native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), 64, 256,
+        _native.check(_native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), 64, 256, 0,
                                                         ctypes.c_uint64(0xDEADBEEF12345678), step, out.data_ptr()))
         ref = sample_actions(m.cpu().numpy(), 0xDEADBEEF12345678, step)
         np.testing.assert_array_equal(out.cpu().numpy(), ref)
@@ -279,7 +279,7 @@ def test_device_sampler_ragged_rows(rows):
     m[0, ::3] = 0   # rows with no valid entry use the uniform fallback
     md = torch.from_numpy(m).cuda()
     out = torch.full((1, rows, 7), -1, dtype=torch.int64, device="cuda")
-    _native.check(_native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, md.data_ptr(), 1, rows,
+    _native.check(_native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, md.data_ptr(), 1, rows, 0,
                                                     ctypes.c_uint64(42), 7, out.data_ptr()))
     np.testing.assert_array_equal(out.cpu().numpy(), sample_actions(m, 42, 7))
 
@@ -340,7 +340,7 @@ def test_no_invariant_violation_long_run():
     act = torch.empty((1024, 256, 7), dtype=torch.int64, device=g.device)
     for s in range(2000):
         m = g.get_action_mask()
-        _native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), 1024, 256, 77, s, act.data_ptr())
+        _native.lib().mrts_sample_actions(torch.cuda.current_stream().cuda_stream, m.data_ptr(), 1024, 256, 0, 77, s, act.data_ptr())
         obs, r, d, _ = g.step(act)
     torch.cuda.synchronize()
     assert g.error_flags() == 0

@@ -1,0 +1,127 @@
+"""Multi-GPU sharding is exact ("per-shard results equal
+single-GPU results for the same env indices"; §8e: envs shard with no
+collective).  A shard holds global envs [env0, env0 + n) and games
+[game_offset, ...): the sampler's Philox counter takes the global env index and
+the random bots' streams the global game index, so each shard plays exactly its
+slice of one unsharded run.
+
+* in process: two shard engines of n envs == one engine of 2n envs, every step;
+* end to end: bench.py's own sharding path under torch.distributed.run with 2
+  ranks (gloo: both share the box's one GPU) == one bench.py process of 2n envs.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+
+
+def _env(nsp, nbot, bots, game_offset, max_steps):
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+
+    return MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=max_steps,
+                                  map_paths=["maps/16x16/basesWorkers16x16.xml"], ai2s=[getattr(microrts_ai, b) for b in bots],
+                                  reward_weight=W, return_tensors=True, obs_dtype=torch.int32, game_offset=game_offset)
+
+
+@pytest.mark.parametrize("kind", ["selfplay", "bots"])
+def test_two_shards_equal_one_run(kind):
+    import ctypes
+
+    import torch
+
+    from gym_microrts import _native
+
+    n, max_steps, steps = 256, 90, 200
+    bots = (["randomBiasedAI", "randomAI", "coacAI", "workerRushAI"] * (2 * n))[:2 * n] if kind == "bots" else []
+    nsp = 2 * n if kind == "selfplay" else 0
+    g_per_env = 0.5 if kind == "selfplay" else 1
+    whole = _env(nsp, len(bots), bots, 0, max_steps)
+    shards = [_env(nsp // 2, len(bots) // 2, bots[r * n:(r + 1) * n] if bots else [], int(r * n * g_per_env), max_steps)
+              for r in range(2)]
+    envs = [whole] + shards
+    for e in envs:
+        e.reset()
+    lib, st = _native.lib(), torch.cuda.current_stream().cuda_stream
+    acts = [torch.empty((e.num_envs, 256, 7), dtype=torch.int64, device="cuda") for e in envs]
+    env0s = [0, 0, n]
+    resets = 0
+    for s in range(steps):
+        out = []
+        for e, a, e0 in zip(envs, acts, env0s):
+            m = e.get_action_mask()
+            _native.check(lib.mrts_sample_actions_src(st, m.data_ptr(), e.source_unit_mask.data_ptr(), e.num_envs, 256, e0,
+                                                      ctypes.c_uint64(77), s, a.data_ptr()))
+            o, r, d, i = e.step(a)
+            out.append((o.clone(), r.clone(), d.clone(), i._raw.clone(), e._mask.clone()))
+        for k in range(5):
+            assert torch.equal(out[0][k], torch.cat([out[1][k], out[2][k]])), f"step {s} output {k}"
+        resets += int(out[0][2].sum())
+    assert resets >= 2 * n
+    for e in envs:
+        assert e.error_flags() == 0
+
+
+def test_sampler_env_offset_matches_oracle():
+    import ctypes
+
+    import torch
+
+    from gym_microrts import _native
+    from oracle_py import sample_actions
+
+    rng = np.random.default_rng(3)
+    m = (rng.random((40, 64, 78)) < 0.2).astype(np.int32)
+    src = (m.sum(-1) > 0).astype(np.int32)
+    md, sd = torch.from_numpy(m).cuda(), torch.from_numpy(src).cuda()
+    out = torch.empty((40, 64, 7), dtype=torch.int64, device="cuda")
+    for env0 in (0, 1, 4096, 123457):
+        _native.check(_native.lib().mrts_sample_actions_src(torch.cuda.current_stream().cuda_stream, md.data_ptr(), sd.data_ptr(), 40,
+                                                            64, env0, ctypes.c_uint64(9), 5, out.data_ptr()))
+        ref = sample_actions(m, 9, 5, env0=env0)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    # a shard's rows are the slice of the whole batch's
+    np.testing.assert_array_equal(sample_actions(m[20:], 9, 5, env0=20), sample_actions(m, 9, 5)[20:])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+def test_bench_sharding_end_to_end(tmp_path):
+    """bench.py --gpus 2 over torch.distributed.run (2 ranks, gloo) dumps each rank's
+    final outputs; they are the two halves of a 1-rank bench.py run of twice the
+    envs (same seed, staggered pre-roll, warmup and timed steps)."""
+    common = ["--steps", "25", "--warmup", "3", "--preroll", "120", "--max-steps", "120", "--no-cpu-baseline",
+              "--no-kernel-events"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+                          "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+                          "--envs-per-gpu", "256", "--dist-backend", "gloo", "--dump", str(tmp_path / "two")] + common,
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert two.returncode == 0, two.stderr[-3000:]
+    one = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--envs-per-gpu", "512", "--dump", str(tmp_path / "one")]
+                         + common, env=env, capture_output=True, text=True, timeout=240)
+    assert one.returncode == 0, one.stderr[-3000:]
+    import json
+
+    line = json.loads(two.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["window"]["auto_resets"] > 0
+    whole = np.load(tmp_path / "one.rank0.npz")
+    parts = [np.load(tmp_path / f"two.rank{r}.npz") for r in range(2)]
+    for k in ("obs", "mask", "src", "raw", "done", "stats"):
+        np.testing.assert_array_equal(whole[k], np.concatenate([p[k] for p in parts]), err_msg=k)
