@@ -66,8 +66,8 @@ struct BL {   // LDS of one bot game
 __host__ __device__ inline size_t b16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ inline size_t bot_lds_bytes(int HW, int W) {
     const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
-    return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW) + 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) +
-           b16((size_t)HW) + b16(4 * 32);
+    return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW) + b16((size_t)HW) + 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) +
+           b16(4 * 32);
 }
 
 __device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W) {
@@ -82,10 +82,10 @@ __device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W) {
     L.uuid = (int32_t*)take(4 * (size_t)HW);
     L.pa = (int32_t*)take(4 * (size_t)HW);
     L.aa = (int4*)take(32 * (size_t)HW);
+    L.wall = (uint8_t*)take((size_t)HW);   // at the step kernel's wall offset too (wall_shared)
     L.pend = (uint32_t*)take(4 * posw);
     L.pab = (uint32_t*)take(4 * posw);
     L.vis = (uint32_t*)take(4 * ((size_t)HW / 32 + 1));
-    L.wall = (uint8_t*)take((size_t)HW);
     L.sc = (int*)take(4 * 32);
     return L;
 }
@@ -102,6 +102,21 @@ struct BS {
     int pa_res[2];
     uint32_t frow;  // lane y: free cells of row y (no wall, no visible unit)
     uint32_t rurow; // lane y: PlayerAction positions in row y (path finding's ResourceUsage)
+    // n <= 64: the unit list lives in registers, entry k in lane k (0 / INT_MIN past the list)
+    int kcell;      // cell of unit k
+    int kuid;       // its uid
+    uint32_t kunit; // its unit word (the bot's view)
+    uint32_t kact;  // its pending action word
+    int kenemy;     // list index of unit k's closest enemy (-1: none), for the behaviours
+    // naa <= 64: abstract action k (both int4 words) in lane k; the LDS list is kept too
+    int4 kA, kB;
+};
+
+// one unit of the list, read from the registers (or LDS past 64 units)
+struct URef {
+    int k;          // list index (pgs.units order)
+    int c, uid;
+    uint32_t u;     // unit word
 };
 
 __device__ __forceinline__ bool lane0() { return threadIdx.x == 0; }
@@ -114,43 +129,124 @@ __device__ __forceinline__ bool v_free(const BS& S, const BL& L, int x, int y) {
     return !L.wall[c] && L.unit[c] == 0;
 }
 
-// uid -> cell in the bot's view (binary search over the uid-ordered list), -1 if absent
-__device__ __forceinline__ int cell_of_uid(const BS& S, const BL& L, int uid) {
-    int lo = 0, hi = S.n - 1;
-    while (lo <= hi) {
-        int mid = (lo + hi) >> 1, v = L.uuid[mid];
-        if (v == uid) return L.ucell[mid];
-        if (v < uid) lo = mid + 1;
-        else hi = mid - 1;
+// ---- cross-lane moves without LDS: DPP and scalar lane reads ---------------------
+// The bot is one wave whose decisions are a long chain of dependent steps, so
+// every cross-lane step is on the critical path: ds_bpermute (__shfl) costs an
+// LDS round trip, DPP and v_readlane a few VALU cycles.
+__device__ __forceinline__ uint32_t from_lane_below(uint32_t v) {   // lane l <- lane l-1, lane 0 <- 0 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_lane_above(uint32_t v) {   // lane l <- lane l+1, lane 63 <- 0 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int lane_value(int v, int lane) {   // v of lane `lane` (wave-uniform index)
+    return __builtin_amdgcn_readlane(v, lane);
+}
+// wave-wide unsigned minimum: DPP prefix minima inside each 16-lane row, then the four rows' last lanes
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
+    const uint32_t a = (uint32_t)lane_value((int)v, 15), b = (uint32_t)lane_value((int)v, 31);
+    const uint32_t c = (uint32_t)lane_value((int)v, 47), d = (uint32_t)lane_value((int)v, 63);
+    return min(min(a, b), min(c, d));
+}
+
+// uid -> cell in the bot's view, -1 if absent: one compare per lane over the
+// uid-ordered list (registers when it fits the wave), a ballot and a lane read.
+// With `act`: the unit's pending action word too.
+__device__ __forceinline__ int cell_of_uid(const BS& S, const BL& L, int uid, uint32_t* act = nullptr) {
+    if (S.n <= BT) {
+        const unsigned long long m = __ballot(S.kuid == uid);
+        if (!m) return -1;
+        if (act) *act = (uint32_t)lane_value((int)S.kact, __builtin_ctzll(m));
+        return lane_value(S.kcell, __builtin_ctzll(m));
+    }
+    for (int base = 0; base < S.n; base += BT) {
+        const int k = base + threadIdx.x;
+        const unsigned long long m = __ballot(k < S.n && L.uuid[k] == uid);
+        if (m) {
+            const int c = L.ucell[base + __builtin_ctzll(m)];
+            if (act) *act = L.act[c];
+            return c;
+        }
     }
     return -1;
 }
 
 // ---- wave-parallel scans of the unit list (results identical in every lane) ----
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long k) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long v = __shfl_xor(k, o);
-        k = v < k ? v : k;
+// Predicates see (cell, unit word, action word) of one list entry per lane.
+__device__ __forceinline__ void list_entry(const BS& S, const BL& L, int k, int& c, uint32_t& u, uint32_t& a) {
+    if (S.n <= BT) {
+        c = S.kcell;
+        u = S.kunit;
+        a = S.kact;
+    } else {
+        c = k < S.n ? L.ucell[k] : 0;
+        u = k < S.n ? L.unit[c] : 0u;
+        a = k < S.n ? L.act[c] : 0u;
     }
-    return k;
 }
 // The first unit in pgs.units order (a serial `d < best` scan) among those
-// `want` selects minimising the Manhattan distance to (x, y): min over
-// (distance, list index) across the lanes.  -1 if none; *dist = that distance.
+// `want` selects minimising the Manhattan distance to (x, y): min over the
+// packed key (distance << 16 | list index) across the lanes.  -1 if none;
+// *dist = that distance.
+template <typename F>
+__device__ __forceinline__ int closest_index(const BS& S, const BL& L, int x, int y, F want, int* dist = nullptr);
+__device__ __forceinline__ URef ref_at(const BS& S, const BL& L, int k) {
+    URef r;
+    r.k = k;
+    if (S.n <= BT) {
+        r.c = lane_value(S.kcell, k);
+        r.uid = lane_value(S.kuid, k);
+        r.u = (uint32_t)lane_value((int)S.kunit, k);
+    } else {
+        r.c = L.ucell[k];
+        r.uid = L.uuid[k];
+        r.u = L.unit[r.c];
+    }
+    return r;
+}
 template <typename F>
 __device__ __forceinline__ int closest_unit(const BS& S, const BL& L, int x, int y, F want, int* dist = nullptr) {
-    unsigned long long key = ~0ull;
+    const int k = closest_index(S, L, x, y, want, dist);
+    return k < 0 ? -1 : (S.n <= BT ? lane_value(S.kcell, k) : L.ucell[k]);
+}
+// list index of the closest unit `want` selects (see closest_unit), -1 if none
+template <typename F>
+__device__ __forceinline__ int closest_index(const BS& S, const BL& L, int x, int y, F want, int* dist) {
+    uint32_t key = 0xFFFFFFFFu;
     for (int k = threadIdx.x; k < S.n; k += BT) {
-        const int c = L.ucell[k];
-        if (!want(c)) continue;
-        const unsigned d = (unsigned)(iabs(c % S.W - x) + iabs(c / S.W - y));
-        const unsigned long long kk = ((unsigned long long)d << 32) | (unsigned)k;
+        int c;
+        uint32_t u, a;
+        list_entry(S, L, k, c, u, a);
+        if (!want(c, u, a)) continue;
+        const uint32_t d = (uint32_t)(iabs(c % S.W - x) + iabs(c / S.W - y));
+        const uint32_t kk = (d << 16) | (uint32_t)k;
         key = kk < key ? kk : key;
     }
-    key = wave_min_u64(key);
-    if (key == ~0ull) return -1;
-    if (dist) *dist = (int)(key >> 32);
-    return L.ucell[(int)(key & 0xFFFFFFFFu)];
+    key = wave_min_u32(key);
+    if (key == 0xFFFFFFFFu) return -1;
+    if (dist) *dist = (int)(key >> 16);
+    return (int)(key & 0xFFFFu);
+}
+// body(cell) for every unit of the list `want` selects, in pgs.units order.
+// `want` must not depend on what `body` changes (abstract actions, the PlayerAction).
+template <typename P, typename F>
+__device__ __forceinline__ void for_each_unit(const BS& S, const BL& L, P want, F body) {
+    for (int base = 0; base < S.n; base += BT) {
+        const int k = base + threadIdx.x;
+        int c;
+        uint32_t u, a;
+        list_entry(S, L, k, c, u, a);
+        unsigned long long m = __ballot(k < S.n && want(c, u, a));
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1ull;
+            body(ref_at(S, L, base + j));
+        }
+    }
 }
 // number of units `want` selects
 template <typename F>
@@ -158,20 +254,26 @@ __device__ __forceinline__ int count_where(const BS& S, const BL& L, F want) {
     int n = 0;
     for (int base = 0; base < S.n; base += BT) {
         const int k = base + threadIdx.x;
-        n += __popcll(__ballot(k < S.n && want(L.ucell[k])));
+        int c;
+        uint32_t u, a;
+        list_entry(S, L, k, c, u, a);
+        n += __popcll(__ballot(k < S.n && want(c, u, a)));
     }
     return n;
 }
-// the idx-th unit (pgs.units order) `want` selects, -1 if fewer
+// list index of the idx-th unit (pgs.units order) `want` selects, -1 if fewer
 template <typename F>
-__device__ __forceinline__ int nth_where(const BS& S, const BL& L, int idx, F want) {
+__device__ __forceinline__ int nth_index(const BS& S, const BL& L, int idx, F want) {
     for (int base = 0; base < S.n; base += BT) {
         const int k = base + threadIdx.x;
-        unsigned long long m = __ballot(k < S.n && want(L.ucell[k]));
+        int c;
+        uint32_t u, a;
+        list_entry(S, L, k, c, u, a);
+        unsigned long long m = __ballot(k < S.n && want(c, u, a));
         const int cnt = __popcll(m);
         if (idx < cnt) {
             for (int t = 0; t < idx; t++) m &= m - 1ull;
-            return L.ucell[base + __builtin_ctzll(m)];
+            return base + __builtin_ctzll(m);
         }
         idx -= cnt;
     }
@@ -254,32 +356,59 @@ __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int r
         }
         goal &= fr;
     }
+    // the start's four neighbours as bits of their rows: one ballot per layer
+    // tells whether the front reached any of them (the direction is then read once)
+    uint32_t nbr = 0;
+    if (lane == sy) nbr = ((sx + 1 < S.W) ? 1u << (sx + 1) : 0u) | (sx > 0 ? 1u << (sx - 1) : 0u);
+    if (lane == sy - 1 || lane == sy + 1) nbr = 1u << sx;
+    const uint32_t frm = fr & rowmask;
     uint32_t seen = goal, front = goal;
     for (int it = 0; it <= S.HW; it++) {
-        const uint32_t rU = __shfl(front, max(sy - 1, 0)), rC = __shfl(front, sy), rD = __shfl(front, min(sy + 1, 63));
-        if (sy > 0 && ((rU >> sx) & 1u)) return 0;
-        if (sx + 1 < S.W && ((rC >> (sx + 1)) & 1u)) return 1;
-        if (sy + 1 < S.H && ((rD >> sx) & 1u)) return 2;
-        if (sx > 0 && ((rC >> (sx - 1)) & 1u)) return 3;
-        uint32_t up = __shfl_up(front, 1), dn = __shfl_down(front, 1);
-        if (lane == 0) up = 0;
-        if (lane >= S.H - 1) dn = 0;
-        const uint32_t grow = ((front << 1) | (front >> 1) | up | dn) & rowmask & fr & ~seen;
+        if (__ballot((front & nbr) != 0)) {   // first layer touching a neighbour: ties UP, RIGHT, DOWN, LEFT
+            const uint32_t rU = (uint32_t)lane_value((int)front, max(sy - 1, 0)), rC = (uint32_t)lane_value((int)front, sy),
+                           rD = (uint32_t)lane_value((int)front, min(sy + 1, 63));
+            if (sy > 0 && ((rU >> sx) & 1u)) return 0;
+            if (sx + 1 < S.W && ((rC >> (sx + 1)) & 1u)) return 1;
+            if (sy + 1 < S.H && ((rD >> sx) & 1u)) return 2;
+            return 3;
+        }
+        // rows y-1 and y+1 of the front (rows >= H hold no free cell, so nothing grows there)
+        const uint32_t up = from_lane_below(front), dn = from_lane_above(front);
+        const uint32_t grow = ((front << 1) | (front >> 1) | up | dn) & frm & ~seen;
         seen |= grow;
         front = grow;
-        if (!__any(grow != 0)) return -1;
+        if (!__ballot(grow != 0)) return -1;
     }
     return -1;
 }
 
 // ---- abstract actions ----------------------------------------------------------
+// LinkedHashMap<Unit, AbstractAction> in insertion order: the LDS list is the
+// record; while it holds <= 64 entries, entry k also lives in lane k's kA / kB,
+// and lookups are one ballot / lane read.
 __device__ __forceinline__ int find_aa(const BS& S, const BL& L, int uid) {   // first entry of the unit, lane-parallel
+    if (S.naa <= BT) {
+        const unsigned long long m = __ballot((int)threadIdx.x < S.naa && S.kA.x == uid);
+        return m ? __builtin_ctzll(m) : -1;
+    }
     for (int base = 0; base < S.naa; base += BT) {
         const int k = base + threadIdx.x;
         const unsigned long long m = __ballot(k < S.naa && L.aa[2 * k].x == uid);
         if (m) return base + __builtin_ctzll(m);
     }
     return -1;
+}
+__device__ __forceinline__ int4 lane_int4(int4 v, int k) {
+    return make_int4(lane_value(v.x, k), lane_value(v.y, k), lane_value(v.z, k), lane_value(v.w, k));
+}
+__device__ __forceinline__ void aa_entry(const BS& S, const BL& L, int k, int4& a, int4& b) {
+    if (S.naa <= BT) {
+        a = lane_int4(S.kA, k);
+        b = lane_int4(S.kB, k);
+    } else {
+        a = L.aa[2 * k];
+        b = L.aa[2 * k + 1];
+    }
 }
 __device__ __forceinline__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   // actions.put(u, aa)
     int k = find_aa(S, L, a.x);
@@ -289,6 +418,10 @@ __device__ __forceinline__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   /
             return;
         }
         k = S.naa++;
+    }
+    if ((int)threadIdx.x == k) {
+        S.kA = a;
+        S.kB = b;
     }
     if (lane0()) {
         L.aa[2 * k] = a;
@@ -321,8 +454,7 @@ __device__ __forceinline__ int adj_dir(int ux, int uy, int x, int y) {
 
 __device__ __forceinline__ int train_score(const BS& S, const BL& L, int x, int y, int type, int player) {   // Train.score
     int dist = 0;   // stays 0 when nothing qualifies
-    closest_unit(S, L, x, y, [&](int c) {
-        const uint32_t o = L.unit[c];
+    closest_unit(S, L, x, y, [&](int, uint32_t o, uint32_t) {
         return ut_can_harvest(type) ? u_type(o) == RESOURCE : (u_owner(o) >= 0 && u_owner(o) != player);
     }, &dist);
     return -dist;
@@ -417,14 +549,15 @@ __device__ __forceinline__ void translate_actions(BS& S, const BL& L) {
     int w = 0;
     const int n0 = S.naa;
     for (int k = 0; k < n0; k++) {
-        int4 a = L.aa[2 * k];
-        const int4 b = L.aa[2 * k + 1];
-        const int cu = cell_of_uid(S, L, a.x);
+        int4 a, b;
+        aa_entry(S, L, k, a, b);
+        uint32_t act = 0;
+        const int cu = cell_of_uid(S, L, a.x, &act);
         const bool del = cu < 0 || aa_completed(S, L, a, cu);
-        if (!del && L.act[cu] == 0) {
+        if (!del && act == 0) {
             const int code = aa_execute(S, L, a, b, cu);
             if (code >= 0) {
-                RU r = usage(S, cu, code, u_owner(L.unit[cu]));
+                RU r = usage(S, cu, code, S.player);
                 if (consistent(S, r, L.pab, S.pa_res)) pa_add(S, L, cu, code);
             }
         }
@@ -436,64 +569,63 @@ __device__ __forceinline__ void translate_actions(BS& S, const BL& L) {
             w++;
         }
     }
-    S.naa = w;
+    S.naa = w;   // (the register copy is stale from here on: only the LDS list is written back)
 }
 
 // ---- behaviours ------------------------------------------------------------------
-// closest enemy of the unit at cu: precomputed for every unit in k_bot before
-// the behaviours (L.pa[cell]) for the rush family; wave-parallel scan otherwise
-__device__ __forceinline__ int closest_enemy(const BS& S, const BL& L, int cu, bool table = true) {
-    if (table) return L.pa[cu];
-    const int me = u_owner(L.unit[cu]);
-    return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
-        const int o = u_owner(L.unit[c]);
+// closest enemy of a unit: the table the bot builds before the behaviours (rush
+// family, coacAI), or a wave-parallel scan
+__device__ __forceinline__ int closest_enemy_index(const BS& S, const BL& L, const URef& w, bool table = true) {
+    if (table) return S.n <= BT ? lane_value(S.kenemy, w.k) : L.pa[w.k];
+    const int me = u_owner(w.u);
+    return closest_index(S, L, w.c % S.W, w.c / S.W, [&](int, uint32_t u, uint32_t) {
+        const int o = u_owner(u);
         return o >= 0 && o != me;
     });
 }
-__device__ __forceinline__ int closest_of(const BS& S, const BL& L, int cu, bool want_resource) {
-    const int me = u_owner(L.unit[cu]);
-    return closest_unit(S, L, cu % S.W, cu / S.W, [&](int c) {
-        const uint32_t o = L.unit[c];
+__device__ __forceinline__ int closest_of_index(const BS& S, const BL& L, const URef& w, bool want_resource) {
+    const int me = u_owner(w.u);
+    return closest_index(S, L, w.c % S.W, w.c / S.W, [&](int, uint32_t o, uint32_t) {
         return want_resource ? u_type(o) == RESOURCE : (ut_is_stockpile(u_type(o)) && u_owner(o) == me);
-    });
+    }, nullptr);
 }
 
 // meleeUnitBehavior (+ PO* exploration: nearest cell the player cannot observe)
-__device__ __forceinline__ void melee_behavior(BS& S, const BL& L, int cu, bool po) {
-    const int e = closest_enemy(S, L, cu);
+__device__ __forceinline__ void melee_behavior(BS& S, const BL& L, const URef& w, bool po) {
+    const int e = closest_enemy_index(S, L, w);
     if (e >= 0) {
-        ab_attack(S, L, L.uid[cu], L.uid[e]);
+        ab_attack(S, L, w.uid, ref_at(S, L, e).uid);
         return;
     }
     if (!(po && S.partial)) return;
-    const int ux = cu % S.W, uy = cu / S.W;
-    // first minimum in row-major scan order = min over (d^2, cell)
-    unsigned long long key = ~0ull;
+    const int ux = w.c % S.W, uy = w.c / S.W;
+    // first minimum in row-major scan order = min over (d^2 << 16 | cell); d^2 <= 32^2 + 64^2
+    uint32_t key = 0xFFFFFFFFu;
     for (int c = threadIdx.x; c < S.HW; c += BT) {
         if (bit_at(L.vis, c)) continue;
         const int x = c % S.W, y = c / S.W;
-        const unsigned long long kk = ((unsigned long long)((ux - x) * (ux - x) + (uy - y) * (uy - y)) << 32) | (unsigned)c;
+        const uint32_t kk = ((uint32_t)((ux - x) * (ux - x) + (uy - y) * (uy - y)) << 16) | (uint32_t)c;
         key = kk < key ? kk : key;
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long v = __shfl_xor(key, o);
-        key = v < key ? v : key;
-    }
-    if (key != ~0ull) {
-        const int c = (int)(key & 0xFFFFFFFFu);
-        ab_move(S, L, L.uid[cu], c % S.W, c / S.W);
+    key = wave_min_u32(key);
+    if (key != 0xFFFFFFFFu) {
+        const int c = (int)(key & 0xFFFFu);
+        ab_move(S, L, w.uid, c % S.W, c / S.W);
     }
 }
 
-__device__ __forceinline__ void harvest_behavior(BS& S, const BL& L, int cu) {
-    const int r = closest_of(S, L, cu, true), b = closest_of(S, L, cu, false);
-    if (r < 0 || b < 0) return;
-    const int k = find_aa(S, L, L.uid[cu]);
+// harvest(closest resource, closest own base) unless already harvesting those
+__device__ __forceinline__ void harvest_behavior(BS& S, const BL& L, const URef& w) {
+    const int ri = closest_of_index(S, L, w, true), bi = closest_of_index(S, L, w, false);
+    if (ri < 0 || bi < 0) return;
+    const URef r = ref_at(S, L, ri), b = ref_at(S, L, bi);
+    const int k = find_aa(S, L, w.uid);
     if (k >= 0) {
-        const int4 a = L.aa[2 * k], bb = L.aa[2 * k + 1];
-        if (aa_kind(a) == AA_HARVEST && a.z == L.uid[r] && bb.x == L.uid[b]) return;
+        int4 a, bb;
+        aa_entry(S, L, k, a, bb);
+        if (aa_kind(a) == AA_HARVEST && a.z == r.uid && bb.x == b.uid) return;
     }
-    ab_harvest(S, L, L.uid[cu], L.uid[r], L.uid[b], b);
+    ab_harvest(S, L, w.uid, r.uid, b.uid, b.c);
 }
 
 // AbstractionLayerAI.findBuildingPosition
@@ -521,64 +653,60 @@ __device__ __forceinline__ int find_building_position(const BS& S, const BL& L, 
     return -1;
 }
 
-__device__ __forceinline__ void build_if_not_already(BS& S, const BL& L, int cu, int type, Rsv& rs) {
-    const int k = find_aa(S, L, L.uid[cu]);
+__device__ __forceinline__ void build_if_not_already(BS& S, const BL& L, const URef& w, int type, Rsv& rs) {
+    const int k = find_aa(S, L, w.uid);
     if (k >= 0) {
-        const int4 a = L.aa[2 * k];
+        int4 a, b;
+        aa_entry(S, L, k, a, b);
         if (aa_kind(a) == AA_BUILD && aa_utype(a) == type) return;
     }
-    const int pos = find_building_position(S, L, rs, cu % S.W, cu / S.W);
-    ab_build(S, L, L.uid[cu], type, pos % S.W, pos / S.W);   // C/Java division: -1 -> (-1, 0)
+    const int pos = find_building_position(S, L, rs, w.c % S.W, w.c / S.W);
+    ab_build(S, L, w.uid, type, pos % S.W, pos / S.W);   // C/Java division: -1 -> (-1, 0)
     if (rs.n == 0) rs.a = pos;
     else rs.b = pos;
     rs.n++;
 }
 
+// unit selectors for for_each_unit: the player's idle units of a type / idle army units
+__device__ __forceinline__ auto idle_own(const BS& S, const BL& L, int type) {
+    return [&S, type](int, uint32_t u, uint32_t a) { return u_type(u) == type && u_owner(u) == S.player && a == 0; };
+}
+__device__ __forceinline__ auto idle_own_army(const BS& S, const BL& L) {
+    return [&S](int, uint32_t u, uint32_t a) {
+        const int t = u_type(u);
+        return ut_can_attack(t) && !ut_can_harvest(t) && u_owner(u) == S.player && a == 0;
+    };
+}
+
 __device__ __forceinline__ int count_units(const BS& S, const BL& L, int type, bool own) {
-    return count_where(S, L, [&](int c) {
-        const uint32_t o = L.unit[c];
+    return count_where(S, L, [&](int, uint32_t o, uint32_t) {
         return u_type(o) == type && (own ? u_owner(o) == S.player : (u_owner(o) >= 0 && u_owner(o) != S.player));
     });
 }
 
 // WorkerRush / LightRush / HeavyRush / RangedRush (+ PO*)
+__device__ __forceinline__ void behaviours_parallel(BS& S, const BL& L, int army, bool po, bool coac);
 __device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bool po) {
+    if (S.n <= BT && S.naa <= BT) {
+        behaviours_parallel(S, L, army, po, false);
+        translate_actions(S, L);
+        return;
+    }
     const int p = S.player, res = p ? S.res[1] : S.res[0];
     const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
               nbarracks = count_units(S, L, BARRACKS, true);
-    for (int k = 0; k < S.n; k++) {   // bases
-        const int c = L.ucell[k];
-        const uint32_t u = L.unit[c];
-        if (u_type(u) != BASE || u_owner(u) != p || L.act[c] != 0) continue;
-        const bool tr = army == WORKER ? res >= ut_cost(WORKER) : nworkers < 1 && res >= ut_cost(WORKER);
-        if (tr) ab_train(S, L, L.uid[c], WORKER);
-    }
-    if (army != WORKER) {   // barracks
-        const int t = army;
-        for (int k = 0; k < S.n; k++) {
-            const int c = L.ucell[k];
-            const uint32_t u = L.unit[c];
-            if (u_type(u) != BARRACKS || u_owner(u) != p || L.act[c] != 0) continue;
-            if (res >= ut_cost(t)) ab_train(S, L, L.uid[c], t);
-        }
-    }
-    for (int k = 0; k < S.n; k++) {   // melee units
-        const int c = L.ucell[k];
-        const uint32_t u = L.unit[c];
-        const int t = u_type(u);
-        if (!ut_can_attack(t) || ut_can_harvest(t) || u_owner(u) != p || L.act[c] != 0) continue;
-        melee_behavior(S, L, c, po);
-    }
+    const bool tr = army == WORKER ? res >= ut_cost(WORKER) : nworkers < 1 && res >= ut_cost(WORKER);
+    if (tr) for_each_unit(S, L, idle_own(S, L, BASE), [&](const URef& b) { ab_train(S, L, b.uid, WORKER); });   // bases
+    if (army != WORKER && res >= ut_cost(army))                                                                // barracks
+        for_each_unit(S, L, idle_own(S, L, BARRACKS), [&](const URef& b) { ab_train(S, L, b.uid, army); });
+    for_each_unit(S, L, idle_own_army(S, L), [&](const URef& m) { melee_behavior(S, L, m, po); });            // melee units
     // workers, busy ones included (the list is the tail of the unit list walk)
-    auto own_worker = [&](int c) {
-        const uint32_t u = L.unit[c];
-        return ut_can_harvest(u_type(u)) && u_owner(u) == p;
-    };
+    auto own_worker = [&](int, uint32_t u, uint32_t) { return ut_can_harvest(u_type(u)) && u_owner(u) == p; };
     const int nf = count_where(S, L, own_worker);
     if (nf > 0) {
         Rsv reserved{0, 0, 0};
         int used = 0, head = 0;   // head: workers taken off the free list
-        auto worker = [&](int idx) { return nth_where(S, L, idx, own_worker); };   // idx-th own worker, pgs.units order
+        auto worker = [&](int idx) { return ref_at(S, L, nth_index(S, L, idx, own_worker)); };   // idx-th own worker
         if (nbases == 0 && head < nf && res >= ut_cost(BASE) + used) {
             build_if_not_already(S, L, worker(head++), BASE, reserved);
             used += ut_cost(BASE);
@@ -602,38 +730,26 @@ __device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bo
 // coac_get_action; its free choices are fixed by league.db's outcomes)
 constexpr int COAC_HARVESTERS_PER_BASE = 2, COAC_EXTRA_WORKERS = 2, COAC_BARRACKS_MIN_WORKERS = 2, COAC_DEFENSE_RADIUS = 8;
 __device__ __forceinline__ void coac_get_action(BS& S, const BL& L) {
+    if (S.n <= BT && S.naa <= BT) {
+        behaviours_parallel(S, L, 0, false, true);
+        translate_actions(S, L);
+        return;
+    }
     const int p = S.player, res = p ? S.res[1] : S.res[0];
     const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
               nbarracks = count_units(S, L, BARRACKS, true);
-    for (int k = 0; k < S.n; k++) {   // bases
-        const int c = L.ucell[k];
-        const uint32_t u = L.unit[c];
-        if (u_type(u) != BASE || u_owner(u) != p || L.act[c] != 0) continue;
-        if (nworkers < COAC_HARVESTERS_PER_BASE * nbases + COAC_EXTRA_WORKERS && res >= ut_cost(WORKER)) ab_train(S, L, L.uid[c], WORKER);
-    }
+    if (nworkers < COAC_HARVESTERS_PER_BASE * nbases + COAC_EXTRA_WORKERS && res >= ut_cost(WORKER))     // bases
+        for_each_unit(S, L, idle_own(S, L, BASE), [&](const URef& b) { ab_train(S, L, b.uid, WORKER); });
     const int t = count_units(S, L, LIGHT, false) > count_units(S, L, RANGED, false) + count_units(S, L, HEAVY, false) ? HEAVY : RANGED;
-    for (int k = 0; k < S.n; k++) {   // barracks
-        const int c = L.ucell[k];
-        const uint32_t u = L.unit[c];
-        if (u_type(u) != BARRACKS || u_owner(u) != p || L.act[c] != 0) continue;
-        if (res >= ut_cost(t)) ab_train(S, L, L.uid[c], t);
-    }
-    for (int k = 0; k < S.n; k++) {   // army
-        const int c = L.ucell[k];
-        const uint32_t u = L.unit[c];
-        const int ty = u_type(u);
-        if (!ut_can_attack(ty) || ut_can_harvest(ty) || u_owner(u) != p || L.act[c] != 0) continue;
-        melee_behavior(S, L, c, false);
-    }
-    auto own_worker = [&](int c) {
-        const uint32_t u = L.unit[c];
-        return ut_can_harvest(u_type(u)) && u_owner(u) == p;
-    };
+    if (res >= ut_cost(t))                                                                                    // barracks
+        for_each_unit(S, L, idle_own(S, L, BARRACKS), [&](const URef& b) { ab_train(S, L, b.uid, t); });
+    for_each_unit(S, L, idle_own_army(S, L), [&](const URef& m) { melee_behavior(S, L, m, false); });       // army
+    auto own_worker = [&](int, uint32_t u, uint32_t) { return ut_can_harvest(u_type(u)) && u_owner(u) == p; };
     const int nf = count_where(S, L, own_worker);
     if (nf > 0) {
         Rsv reserved{0, 0, 0};
         int used = 0, head = 0;
-        auto worker = [&](int idx) { return nth_where(S, L, idx, own_worker); };
+        auto worker = [&](int idx) { return ref_at(S, L, nth_index(S, L, idx, own_worker)); };
         if (nbases == 0 && head < nf && res >= ut_cost(BASE) + used) {
             build_if_not_already(S, L, worker(head++), BASE, reserved);
             used += ut_cost(BASE);
@@ -644,20 +760,229 @@ __device__ __forceinline__ void coac_get_action(BS& S, const BL& L) {
         }
         const int nh = COAC_HARVESTERS_PER_BASE * (nbases > 0 ? nbases : 1);
         for (int k = head; k < nf; k++) {
-            const int w = worker(k);
+            const URef w = worker(k);
             if (k - head < nh) {
                 harvest_behavior(S, L, w);
                 continue;
             }
             // defenders: the closest enemy when it is near the worker's closest own base
-            const int e = closest_enemy(S, L, w);
-            if (e < 0) continue;
-            const int b = closest_of(S, L, w, false);
-            if (b < 0 || iabs(b % S.W - e % S.W) + iabs(b / S.W - e / S.W) <= COAC_DEFENSE_RADIUS) ab_attack(S, L, L.uid[w], L.uid[e]);
+            const int ei = closest_enemy_index(S, L, w);
+            if (ei < 0) continue;
+            const int bi = closest_of_index(S, L, w, false);
+            const URef e = ref_at(S, L, ei);
+            const int bc = bi < 0 ? -1 : ref_at(S, L, bi).c;
+            if (bi < 0 || iabs(bc % S.W - e.c % S.W) + iabs(bc / S.W - e.c / S.W) <= COAC_DEFENSE_RADIUS) ab_attack(S, L, w.uid, e.uid);
             else harvest_behavior(S, L, w);
         }
     }
     translate_actions(S, L);
+}
+
+// ---- lane-parallel behaviours (the rush family and coacAI, <= 64 units) --------
+// The behaviours above visit the player's units one after another, each decision
+// a chain of wave-wide steps.  No decision reads another unit's decision: a unit
+// reads the fixed state and only its own abstract action, and at most one
+// behaviour puts an entry for it in a tick.  So every unit decides in its own
+// lane at once, and the puts are then applied as the serial loops would: an
+// existing key is replaced in place, new keys are appended in visiting order
+// (bases, barracks, army, workers; pgs.units order within each).  Only the at
+// most two building workers (findBuildingPosition + its reservations) decide
+// serially, before the rest.  Bit-identical to the serial behaviours (and so
+// to the oracle); used while the unit list and the abstract-action list fit a
+// wave.
+struct LaneDecision {
+    int cat;       // visiting category of the put: 0 bases, 1 barracks, 2 army, 3 workers; -1 = no put
+    int4 a, b;     // the entry put
+    bool explore;  // PO* exploration: target decided afterwards (serially: a full-map scan each)
+};
+__device__ __forceinline__ int lane_gather(int v, int src) { return __shfl(v, src); }   // per-lane source lane
+
+// the player's units that are stockpiles / resources, nearest to this lane's unit (list index, -1 none)
+__device__ __forceinline__ int lane_closest(const BS& S, unsigned long long cand) {
+    const int ux = S.kcell % S.W, uy = S.kcell / S.W;
+    uint32_t key = 0xFFFFFFFFu;
+    while (cand) {
+        const int j = __builtin_ctzll(cand);
+        cand &= cand - 1ull;
+        const int c = lane_value(S.kcell, j);
+        const uint32_t kk = ((uint32_t)(iabs(c % S.W - ux) + iabs(c / S.W - uy)) << 16) | (uint32_t)j;
+        key = kk < key ? kk : key;
+    }
+    return key == 0xFFFFFFFFu ? -1 : (int)(key & 0xFFFFu);
+}
+
+// army: 0 = coacAI (its own worker / army rules), else the rush's army unit type
+__device__ __forceinline__ void behaviours_parallel(BS& S, const BL& L, int army, bool po, bool coac) {
+    const int lane = threadIdx.x, p = S.player, res = p ? S.res[1] : S.res[0];
+    const bool valid = lane < S.n;
+    const uint32_t u = S.kunit;
+    const int t = u_type(u), ow = u_owner(u);
+    const bool own = valid && ow == p, idle = own && S.kact == 0;
+    const unsigned long long own_workers = __ballot(own && ut_can_harvest(t));
+    const int nworkers = __popcll(__ballot(own && t == WORKER)), nbases = __popcll(__ballot(own && t == BASE)),
+              nbarracks = __popcll(__ballot(own && t == BARRACKS)), nf = __popcll(own_workers);
+    // this lane's existing abstract action (keys are unique)
+    int ek = -1;
+    int4 ea = make_int4(0, 0, 0, 0), eb = make_int4(0, 0, 0, 0);
+    for (int j = 0; j < S.naa; j++) {   // (lane reads outside the divergent branch)
+        const int4 aj = lane_int4(S.kA, j), bj = lane_int4(S.kB, j);
+        if (own && aj.x == S.kuid && ek < 0) {
+            ek = j;
+            ea = aj;
+            eb = bj;
+        }
+    }
+    LaneDecision d{-1, make_int4(0, 0, 0, 0), make_int4(-1, 0, 0, 0), false};
+    const int rank = __popcll(own_workers & ((1ull << lane) - 1ull));   // position among the player's workers
+    // builders (serial): base first, then (not WorkerRush) barracks
+    Rsv reserved{0, 0, 0};
+    int used = 0, head = 0;
+    auto build = [&](int type) {
+        const int k = nth_index(S, L, head, [&](int, uint32_t uu, uint32_t) { return ut_can_harvest(u_type(uu)) && u_owner(uu) == p; });
+        const URef w = ref_at(S, L, k);
+        const int e = find_aa(S, L, w.uid);
+        bool skip = false;
+        if (e >= 0) {
+            int4 a0, b0;
+            aa_entry(S, L, e, a0, b0);
+            skip = aa_kind(a0) == AA_BUILD && aa_utype(a0) == type;
+        }
+        if (!skip) {
+            const int pos = find_building_position(S, L, reserved, w.c % S.W, w.c / S.W);
+            if (lane == k) {
+                d.cat = 3;
+                d.a = make_int4(w.uid, AA_BUILD | (type << 4), -1, pk_xy(pos % S.W, pos / S.W));   // Java division: -1 -> (-1, 0)
+                d.b = make_int4(-1, 0, 0, 0);
+            }
+            if (reserved.n == 0) reserved.a = pos;
+            else reserved.b = pos;
+            reserved.n++;
+        }
+        head++;
+    };
+    if (nf > 0 && nbases == 0 && res >= ut_cost(BASE)) {
+        build(BASE);
+        used += ut_cost(BASE);
+    }
+    if (army != WORKER && nf > head && nbarracks == 0 && res >= ut_cost(BARRACKS) + used &&
+        (!coac || nworkers >= COAC_BARRACKS_MIN_WORKERS)) {
+        build(BARRACKS);
+        used += ut_cost(BARRACKS);
+    }
+    // every other unit in its lane
+    const int tarmy = coac ? (__popcll(__ballot(valid && ow >= 0 && ow != p && t == LIGHT)) >
+                                      __popcll(__ballot(valid && ow >= 0 && ow != p && t == RANGED)) +
+                                          __popcll(__ballot(valid && ow >= 0 && ow != p && t == HEAVY))
+                                  ? HEAVY : RANGED)
+                           : army;
+    const bool base_train = coac ? (nworkers < COAC_HARVESTERS_PER_BASE * nbases + COAC_EXTRA_WORKERS && res >= ut_cost(WORKER))
+                                 : (army == WORKER ? res >= ut_cost(WORKER) : nworkers < 1 && res >= ut_cost(WORKER));
+    const int enemy = S.kenemy;
+    const int enemy_uid = lane_gather(S.kuid, max(enemy, 0));
+    const int enemy_cell = lane_gather(S.kcell, max(enemy, 0));
+    const unsigned long long resources = __ballot(valid && t == RESOURCE), stockpiles = __ballot(own && ut_is_stockpile(t));
+    int ri = -1, bi = -1;
+    if (own && ut_can_harvest(t)) {
+        ri = lane_closest(S, resources);
+        bi = lane_closest(S, stockpiles);
+    }
+    const int r_uid = lane_gather(S.kuid, max(ri, 0)), b_uid = lane_gather(S.kuid, max(bi, 0)), b_cell = lane_gather(S.kcell, max(bi, 0));
+    auto harvest = [&]() {
+        if (ri < 0 || bi < 0) return;
+        if (ek >= 0 && aa_kind(ea) == AA_HARVEST && ea.z == r_uid && eb.x == b_uid) return;
+        d.cat = 3;
+        d.a = make_int4(S.kuid, AA_HARVEST, r_uid, 0);
+        d.b = make_int4(b_uid, pk_xy(b_cell % S.W, b_cell / S.W), 0, 0);
+    };
+    auto melee = [&](int cat) {
+        if (enemy >= 0) {
+            d.cat = cat;
+            d.a = make_int4(S.kuid, AA_ATTACK, enemy_uid, 0);
+            d.b = make_int4(-1, 0, 0, 0);
+        } else if (po && S.partial) {
+            d.cat = cat;
+            d.explore = true;
+        }
+    };
+    if (idle && t == BASE) {
+        if (base_train) {
+            d.cat = 0;
+            d.a = make_int4(S.kuid, AA_TRAIN | (WORKER << 4), -1, 0);
+        }
+    } else if (idle && t == BARRACKS) {
+        if (army != WORKER && res >= ut_cost(tarmy)) {
+            d.cat = 1;
+            d.a = make_int4(S.kuid, AA_TRAIN | (tarmy << 4), -1, 0);
+        }
+    } else if (idle && ut_can_attack(t) && !ut_can_harvest(t)) {
+        melee(2);
+    } else if (own && ut_can_harvest(t) && rank >= head) {
+        if (coac) {
+            const int nh = COAC_HARVESTERS_PER_BASE * (nbases > 0 ? nbases : 1);
+            if (rank - head < nh) {
+                harvest();
+            } else if (enemy >= 0) {   // defenders
+                if (bi < 0 || iabs(b_cell % S.W - enemy_cell % S.W) + iabs(b_cell / S.W - enemy_cell / S.W) <= COAC_DEFENSE_RADIUS) {
+                    d.cat = 3;
+                    d.a = make_int4(S.kuid, AA_ATTACK, enemy_uid, 0);
+                    d.b = make_int4(-1, 0, 0, 0);
+                } else {
+                    harvest();
+                }
+            }
+        } else if (army == WORKER) {
+            if (rank == head) harvest();
+            else melee(3);
+        } else {
+            harvest();
+        }
+    }
+    // PO* exploration targets: the nearest cell the player cannot observe (row-major first)
+    unsigned long long ex = __ballot(d.explore);
+    while (ex) {
+        const int j = __builtin_ctzll(ex);
+        ex &= ex - 1ull;
+        const int cj = lane_value(S.kcell, j), ux = cj % S.W, uy = cj / S.W;
+        uint32_t key = 0xFFFFFFFFu;
+        for (int c = lane; c < S.HW; c += BT) {
+            if (bit_at(L.vis, c)) continue;
+            const int x = c % S.W, y = c / S.W;
+            const uint32_t kk = ((uint32_t)((ux - x) * (ux - x) + (uy - y) * (uy - y)) << 16) | (uint32_t)c;
+            key = kk < key ? kk : key;
+        }
+        key = wave_min_u32(key);
+        if (lane == j) {
+            if (key == 0xFFFFFFFFu) {
+                d.cat = -1;
+            } else {
+                const int c = (int)(key & 0xFFFFu);
+                d.a = make_int4(S.kuid, AA_MOVE, -1, pk_xy(c % S.W, c / S.W));
+                d.b = make_int4(-1, 0, 0, 0);
+            }
+        }
+    }
+    // apply the puts: replace in place, append new keys in visiting order
+    const bool put = d.cat >= 0, fresh = put && ek < 0;
+    int pos = ek, appended = 0;
+    for (int cat = 0; cat < 4; cat++) {
+        const unsigned long long m = __ballot(fresh && d.cat == cat);
+        if (fresh && d.cat == cat) pos = S.naa + appended + __popcll(m & ((1ull << lane) - 1ull));
+        appended += __popcll(m);
+    }
+    if (S.naa + appended > S.HW) {   // more live entries than cells: cannot happen on legal states
+        if (lane0()) L.sc[2] |= MRTS_ERR_BOT_OVERFLOW;
+        return;
+    }
+    if (put) {
+        L.aa[2 * pos] = d.a;
+        L.aa[2 * pos + 1] = d.b;
+    }
+    S.naa += appended;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (S.naa <= BT) {
+        S.kA = lane < S.naa ? L.aa[2 * lane] : make_int4((int)0x80000000, 0, 0, 0);
+        S.kB = lane < S.naa ? L.aa[2 * lane + 1] : make_int4(0, 0, 0, 0);
+    }
 }
 
 // ---- RandomBiasedAI ------------------------------------------------------------------
@@ -728,13 +1053,11 @@ __device__ __forceinline__ void random_biased_get_action(BS& S, const BL& L) {
     S.pa_res[1] = S.pend_res[1];
     const int posw = (S.HW + 2 * S.W) / 32 + 1;
     for (int i = threadIdx.x; i < posw; i += BT) L.pab[i] = L.pend[i];
-    for (int k = 0; k < S.n; k++) {
-        const int c = L.ucell[k];
-        const uint32_t u = L.unit[c];
-        if (u_owner(u) != S.player || L.act[c] != 0) continue;
+    for_each_unit(S, L, [&](int, uint32_t u, uint32_t a) { return u_owner(u) == S.player && a == 0; }, [&](const URef& ur) {
+        const int c = ur.c;
         int total = 0;
         unit_actions(S, L, c, [&](int, int w) { total += w; });
-        uint32_t ctr[4] = {(uint32_t)L.uid[c], S.tick, (uint32_t)S.game, 0x52414E44u + (uint32_t)(1 - S.player)};
+        uint32_t ctr[4] = {(uint32_t)ur.uid, S.tick, (uint32_t)S.game, 0x52414E44u + (uint32_t)(1 - S.player)};
         philox_b(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
         int t = (int)(((uint64_t)ctr[0] * (uint32_t)total) >> 32), pick = -1;
         unit_actions(S, L, c, [&](int code, int w) {
@@ -747,7 +1070,7 @@ __device__ __forceinline__ void random_biased_get_action(BS& S, const BL& L) {
         RU r = usage(S, c, pick, S.player);
         if (consistent(S, r, L.pab, S.pa_res)) pa_add(S, L, c, pick);
         else pa_add(S, L, c, code_make(A_NONE, 10, 0));
-    }
+    });
 }
 
 
@@ -755,8 +1078,8 @@ __device__ __forceinline__ void random_biased_get_action(BS& S, const BL& L) {
 // random_single_get_action): nothing while a unit of the player is busy, else
 // one idle unit drawn uniformly gets a RandomBiasedAI-weighted action
 __device__ __forceinline__ void random_single_get_action(BS& S, const BL& L) {
-    auto own = [&](int c) { return u_owner(L.unit[c]) == S.player; };
-    if (count_where(S, L, [&](int c) { return own(c) && L.act[c] != 0; }) > 0) return;
+    auto own = [&](int, uint32_t u, uint32_t) { return u_owner(u) == S.player; };
+    if (count_where(S, L, [&](int, uint32_t u, uint32_t a) { return u_owner(u) == S.player && a != 0; }) > 0) return;
     const int ni = count_where(S, L, own);
     if (ni == 0) return;
     S.pa_res[0] = S.pend_res[0];
@@ -766,7 +1089,7 @@ __device__ __forceinline__ void random_single_get_action(BS& S, const BL& L) {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     uint32_t ctr[4] = {0xFFFFFFFFu, S.tick, (uint32_t)S.game, 0x52534E47u + (uint32_t)(1 - S.player)};
     philox_b(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
-    const int c = nth_where(S, L, (int)(((uint64_t)ctr[1] * (uint32_t)ni) >> 32), own);
+    const int c = ref_at(S, L, nth_index(S, L, (int)(((uint64_t)ctr[1] * (uint32_t)ni) >> 32), own)).c;
     int total = 0;
     unit_actions(S, L, c, [&](int, int w) { total += w; });
     int t = (int)(((uint64_t)ctr[0] * (uint32_t)total) >> 32), pick = -1;
@@ -800,8 +1123,17 @@ __device__ __forceinline__ void bot_sync() {
 // workgroup for the NEXT tick while the other waves stream the outputs (no
 // workgroup barriers here then; the game state was stored before the caller's
 // last barrier); otherwise the body of k_bot (a one-wave workgroup).
+// the bot's wall array lies where the step kernel's does (its carve: ten arrays
+// of 4*HW bytes and the 16*HW-byte snapshots; the bot's: six of 4*HW and the
+// 32*HW-byte abstract actions): the fused bot reads the step's copy
+__host__ __device__ inline bool wall_shared(int HW) {
+    return 10 * b16(4 * (size_t)HW) + b16(16 * (size_t)HW) == 6 * b16(4 * (size_t)HW) + b16(32 * (size_t)HW);
+}
+
 template <bool FUSED>
-__device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem) {
+__device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem,
+                                         const int32_t* step_sc = nullptr, bool pre_ok = false, int4 pre_aa = int4{0, 0, 0, 0},
+                                         int4 pre_aa2 = int4{0, 0, 0, 0}) {
     const int g = p.nsp_games + b, lane = threadIdx.x;
     const int HW = p.HW, W = p.W;
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
@@ -822,24 +1154,34 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     S.player = player;
     S.partial = p.partial_obs;
     S.game = p.game_offset + g;
-    S.tick = (uint32_t)genv[MRTS_G_TICKS];
-    S.res[0] = genv[MRTS_G_RES0];
-    S.res[1] = genv[MRTS_G_RES1];
-    S.naa = genv[w_aa];
+    // the game's scalars: the step kernel's LDS copy when fused (read before the
+    // bot's first LDS write), else the stored genv
+    const int32_t* gs = FUSED ? step_sc : genv;
+    S.tick = (uint32_t)gs[MRTS_G_TICKS];
+    S.res[0] = gs[MRTS_G_RES0];
+    S.res[1] = gs[MRTS_G_RES1];
+    S.naa = gs[w_aa];
     S.npa = 0;
     S.pa_res[0] = S.pa_res[1] = 0;
-    const int map = genv[MRTS_G_MAP];
+    const int map = gs[MRTS_G_MAP];
     const int posw = (HW + 2 * W) / 32 + 1, visw = HW / 32 + 1;
+    // Fused: the step kernel's unit / uid / act arrays sit at the bot's offsets
+    // (both carves start unit, uid, act of 4*HW bytes at smem 0) and hold the
+    // state it has just stored -- no reload.
+    // Fused, its wall array too (wall_shared), and the first 128 abstract-action
+    // words come prefetched in registers (pre_aa / pre_aa2: words lane, lane + 64).
     for (int c = lane; c < HW; c += BT) {
-        int4 v = p.cells[(size_t)g * HW + c];
-        L.unit[c] = (uint32_t)v.x;
-        L.uid[c] = v.y;
-        L.act[c] = (uint32_t)v.z;
-        L.wall[c] = p.map_wall[(size_t)map * HW + c];
+        if (!FUSED) {
+            int4 v = p.cells[(size_t)g * HW + c];
+            L.unit[c] = (uint32_t)v.x;
+            L.uid[c] = v.y;
+            L.act[c] = (uint32_t)v.z;
+        }
+        if (!FUSED || !wall_shared(HW)) L.wall[c] = p.map_wall[(size_t)map * HW + c];
     }
     for (int i = lane; i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
     for (int i = lane; i < visw; i += BT) L.vis[i] = 0;
-    for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
+    for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = (FUSED && pre_ok && i < 2 * BT) ? (i < BT ? pre_aa : pre_aa2) : aa_g[i];
     if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     bot_sync<FUSED>();
     // cells observable by the bot's player (PartiallyObservableGameState);
@@ -890,7 +1232,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     if (n <= BT) {   // rank by uid with the uids in registers (one per lane)
         const int c = lane < n ? L.pa[lane] : 0, u = lane < n ? L.uid[c] : 0x7fffffff;
         int r = 0;
-        for (int j = 0; j < n; j++) r += __shfl(u, j) < u;
+        for (int j = 0; j < n; j++) r += lane_value(u, j) < u;
         if (lane < n) {
             L.ucell[r] = c;
             L.uuid[r] = u;
@@ -906,6 +1248,12 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     }
     bot_sync<FUSED>();
     S.n = n;
+    S.kcell = lane < n ? L.ucell[lane] : 0;   // the list in registers (used while n <= 64)
+    S.kuid = lane < n ? L.uuid[lane] : (int)0x80000000;
+    S.kunit = lane < n ? L.unit[S.kcell] : 0u;
+    S.kact = lane < n ? L.act[S.kcell] : 0u;
+    S.kA = lane < S.naa ? L.aa[2 * lane] : make_int4((int)0x80000000, 0, 0, 0);
+    S.kB = lane < S.naa ? L.aa[2 * lane + 1] : make_int4(0, 0, 0, 0);
     S.pend_res[0] = L.sc[0];
     S.pend_res[1] = L.sc[1];
     // lane y: free cells of row y, from one ballot per 64 cells (staged in L.pa,
@@ -932,21 +1280,35 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
-    // the closest enemy of every unit (the scan closest_enemy would do, all
-    // units at once; the state is fixed during getAction): L.pa[cell], staged
-    // like the rows above (-1 = none)
-    for (int k = lane; S.ai != MRTS_AI_RANDOM_BIASED && S.ai != MRTS_AI_RANDOM && k < n; k += BT) {
+    // the closest enemy (list index) of each of the player's units, the scan
+    // closest_enemy_index would do, all units at once (the state is fixed during
+    // getAction): in lane k's kenemy, or L.pa[k] past 64 units; -1 = none
+    const bool table = S.ai != MRTS_AI_RANDOM_BIASED && S.ai != MRTS_AI_RANDOM;
+    S.kenemy = -1;
+    if (table && n <= BT) {   // over the opponent's units only (scalar lane reads of their cells)
+        const int ux = S.kcell % W, uy = S.kcell / W;
+        uint32_t key = 0xFFFFFFFFu;
+        unsigned long long m = __ballot(lane < n && u_owner(S.kunit) == 1 - S.player);
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const int c = lane_value(S.kcell, j);
+            const uint32_t kk = ((uint32_t)(iabs(c % W - ux) + iabs(c / W - uy)) << 16) | (uint32_t)j;
+            key = kk < key ? kk : key;
+        }
+        if (lane < n && u_owner(S.kunit) == S.player && key != 0xFFFFFFFFu) S.kenemy = (int)(key & 0xFFFFu);
+    }
+    for (int k = lane; table && n > BT && k < n; k += BT) {
         const int cu = L.ucell[k], me = u_owner(L.unit[cu]), ux = cu % W, uy = cu / W;
-        unsigned long long key = ~0ull;
-        for (int j = 0; j < n; j++) {
+        uint32_t key = 0xFFFFFFFFu;
+        for (int j = 0; me == S.player && j < n; j++) {
             const int c = L.ucell[j];
             const int o = u_owner(L.unit[c]);
             if (o < 0 || o == me) continue;
-            const unsigned d = (unsigned)(iabs(c % W - ux) + iabs(c / W - uy));
-            const unsigned long long kk = ((unsigned long long)d << 32) | (unsigned)j;
+            const uint32_t kk = ((uint32_t)(iabs(c % W - ux) + iabs(c / W - uy)) << 16) | (uint32_t)j;
             key = kk < key ? kk : key;
         }
-        L.pa[cu] = key == ~0ull ? -1 : L.ucell[(int)(key & 0xFFFFFFFFu)];
+        L.pa[k] = key == 0xFFFFFFFFu ? -1 : (int)(key & 0xFFFFu);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     switch (S.ai) {

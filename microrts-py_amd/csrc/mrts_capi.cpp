@@ -314,6 +314,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.map_wall = (const uint8_t *)(h->ws + h->off_mwall);
     p.map_scal = (const int32_t *)(h->ws + h->off_mscal);
     p.G = h->ngames;
+    p.nmaps = (int)h->maps.size();
     p.HW = h->HW;
     p.W = h->W;
     p.H = h->H;

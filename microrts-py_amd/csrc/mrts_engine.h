@@ -12,6 +12,7 @@ struct EngineParams {
     const uint8_t *map_wall;// [maps][HW]
     const int32_t *map_scal;// [maps][MRTS_MAP_SCALARS]
     int G, HW, W, H;
+    int nmaps;              // map templates (1: every game's terrain is map 0's)
     int nsp, nsp_games, max_steps, obs_float, partial_obs;
     const int64_t *actions; // [N][HW][7]
     const int32_t *src;     // [N][HW]

@@ -629,8 +629,11 @@ __device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s
 struct StatePf {
     int4 cell;
     int genv, src0, src1;
+    int bpa0, bpa1;   // bot games: entry `lane` of the bot PlayerActions (player 0 / 1)
+    int4 aa, aa2;     // bot-fused games, lanes < 64: words lane, lane + 64 of the bot's abstract actions
+    int wall;         // single-map batches: this cell's terrain
 };
-template <int NT>
+template <int NT, bool FB>
 __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, StatePf& pf) {
     const Game G = game_of(p, g);
     const int HW = p.HW, c = min((int)threadIdx.x, HW - 1);   // unconditional: counted waits
@@ -638,6 +641,17 @@ __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, Stat
     pf.src0 = p.src[(size_t)G.env0 * HW + c];
     pf.src1 = p.src[(size_t)(G.env0 + G.nviews - 1) * HW + c];
     pf.genv = p.genv[(size_t)g * MRTS_GENV_WORDS + min((int)threadIdx.x, MRTS_GENV_WORDS - 1)];
+    if (!G.selfplay && p.botpa) {   // speculative: the counts arrive with genv
+        const int32_t* bp = p.botpa + (size_t)(g - p.nsp_games) * 2 * HW;
+        pf.bpa0 = p.bot_ai0 ? bp[c] : 0;   // player 0 bots: MicroRTSBotVecEnv only
+        pf.bpa1 = bp[HW + c];
+        if (FB && threadIdx.x < 64) {   // 2 * HW >= 128 words: fusion needs HW > 64
+            const int4* aa = p.aa + ((size_t)(g - p.nsp_games) * 2 + 1) * HW * 2;
+            pf.aa = aa[threadIdx.x];
+            pf.aa2 = aa[64 + threadIdx.x];
+        }
+    }
+    if (p.nmaps == 1) pf.wall = p.map_wall[c];   // else the game's map is known only with genv
 }
 template <int NT>
 __device__ __forceinline__ void commit_game(const EngineParams& p, const Lds& L, const StatePf& pf) {
@@ -650,7 +664,7 @@ __device__ __forceinline__ void commit_game(const EngineParams& p, const Lds& L,
         L.uid[c] = pf.cell.y;
         L.act[c] = (uint32_t)pf.cell.z;
         L.seq[c] = (uint32_t)pf.cell.w;
-        L.wall[c] = p.map_wall[(size_t)map * HW + c];
+        L.wall[c] = p.nmaps == 1 ? (uint8_t)pf.wall : p.map_wall[(size_t)map * HW + c];
     }
     __syncthreads();
 }
@@ -670,7 +684,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
     const int g = blockIdx.x;
-    if (pf_ok) prefetch_game<NT>(p, g, pf);
+    if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
     const Game G = game_of(p, g);
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
     // the source-unit rows of this lane's first cell, fetched in the same round
@@ -731,12 +745,18 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // before this tick's issues: JNIGridnetClient.gameStep order)
     const int npa = (!G.selfplay && p.botpa) ? L.sc[SC_NPA] : 0;
     const int npa0 = bot0 ? L.sc[MRTS_G_NPA0] : 0;
-    for (int i = threadIdx.x; i < npa + npa0; i += NT) {
-        const int q = i < npa ? 1 : 0, k = q ? i : i - npa;
-        const int e = p.botpa[((size_t)(g - p.nsp_games) * 2 + q) * HW + k];
-        const int c = e & 0xFFFF, code = e >> 16;
-        (q ? L.blist : L.blist0)[k] = c;
-        L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, q)) ? LEGAL : 0u) | (uint32_t)code;
+    // entry k of player q's PlayerAction: lane k's prefetched word (maps with HW <= NT),
+    // else a load; its position in the PlayerAction (the LinkedHashMap rank) rides in aux
+    for (int q = 0; q < 2; q++) {
+        const int nq = q ? npa : npa0;
+        for (int k = threadIdx.x; k < nq; k += NT) {
+            const int e = (pf_ok && k == (int)threadIdx.x) ? (q ? pf.bpa1 : pf.bpa0)
+                                                           : p.botpa[((size_t)(g - p.nsp_games) * 2 + q) * HW + k];
+            const int c = e & 0xFFFF, code = e >> 16;
+            (q ? L.blist : L.blist0)[k] = c;
+            L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, q)) ? LEGAL : 0u) | ((uint32_t)k << 12) |
+                       (uint32_t)code;
+        }
     }
     __syncthreads();
     // pending move/produce reservations (ResourceUsage of unitActions)
@@ -754,14 +774,15 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         uint32_t a = L.act[c];
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
     }, L.prod, L.ballot);
-    // (2a) rows that interact with nothing else this tick issue lane-parallel: an
-    //      agent row that is not a produce and, if a move, whose target position
-    //      no other row (either player, bot rows included) and no pending
-    //      assignment claims, while no pending produce is over its owner's budget
-    //      (which would make every new action inconsistent).  Such a row meets no
-    //      candidate in issue() and no other row in fromVectorAction's filter, so
-    //      issuing it out of order is exact: its LinkedHashMap rank is still its
-    //      cell.  Everything else takes the ordered path (2b).
+    // (2a) rows that interact with nothing else this tick issue lane-parallel: a
+    //      row (agent or device bot) that is not a produce and, if a move, whose
+    //      target position no other row (either player) and no pending assignment
+    //      claims, while no pending produce is over its owner's budget (which would
+    //      make every new action inconsistent).  Such a row meets no candidate in
+    //      issue() and no other row in fromVectorAction's filter, and no ordered
+    //      row of the other player meets it, so issuing it out of order is exact:
+    //      its LinkedHashMap rank is still its cell (agent rows) or its position in
+    //      the bot's PlayerAction.  Everything else takes the ordered path (2b).
     {
         const int posw = (HW + 2 * p.W) / 32 + 1;
         for (int i = threadIdx.x; i < 2 * posw; i += NT) L.claim[i] = 0;
@@ -787,7 +808,8 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
                 if (!(nw & CAND)) continue;
                 const uint32_t u = L.unit[c];
                 const int q = u_owner(u);
-                if (!G.selfplay && (q != 0 || bot0)) continue;   // bot rows: ordered path
+                const bool botrow = !G.selfplay && (q != 0 || bot0);
+                const int rank = botrow ? (int)((nw >> 12) & 0xFFFu) : c;
                 const int code = (int)(nw & 0xFFFu), ty = code_type(code);
                 if (ty == A_PRODUCE) continue;
                 int n = -1;
@@ -802,7 +824,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
                 else if (!(nw & LEGAL)) { dur = eta_code(code, u_type(u)); cur = code_make(A_NONE, 0, 0); }
                 const int ct = code_type(cur);
                 L.act[c] = act_make(cur, ct == A_NONE ? time + dur : time + eta_code(cur, u_type(u)));
-                L.seq[c] = seq_make(time, q, c);
+                L.seq[c] = seq_make(time, q, rank);
                 if (ct == A_MOVE) L.resv[n] = c;
                 if (ct == A_HARVEST || ct == A_RETURN) atomicAdd(&L.sc[SC_R0 + 6 * q + 1], 1);
                 if (ct == A_ATTACK) atomicAdd(&L.sc[SC_R0 + 6 * q + 4], 1);
@@ -943,7 +965,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const bool botg = FB && g >= p.nsp_games && NT > 64;
     emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0);
     if (FB && botg && threadIdx.x < 64)   // every read of the stored state is behind phase A's barrier
-        bots::bot_game<true>(p, g - p.nsp_games, 1, smem);   // the step's arrays are dead: only L.outw is read on
+        bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2);   // the step's arrays are dead: only L.outw is read on
 }
 
 // ---------------------------------------------------------------------------
