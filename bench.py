@@ -72,7 +72,8 @@ def parse():
 # The headline metric is "selfplay" (8192 envs / GPU of 16x16 basesWorkers).
 WORKLOADS = {
     "selfplay": (MAP, "all", 0, None, False),
-    "coac": (MAP, 0, "all", "coacAI", False),          # configs[1]: envs vs device-side coacAI
+    "coac": (MAP, 0, "all", "coacAI", False),          # configs[1]: envs vs device-side coacAI (BASELINE.md M3)
+    "passive": (MAP, 0, "all", "passiveAI", False),    # envs vs passiveAI
     "workerrush": (MAP, 0, "all", "workerRushAI", False),
     "partial_obs": (MAP, "all", 0, None, True),       # configs[3]: partial_obs=True, 31 planes
     "8x8": ("maps/8x8/basesWorkers8x8.xml", "all", 0, None, False),
@@ -93,6 +94,8 @@ def stagger_plan(G, ticks, game0=0, G_total=None):
     indices per tick, so shards reset exactly the games one unsharded run would."""
     G_total = G if G_total is None else G_total
     plan = [[] for _ in range(ticks)]
+    if ticks <= 0:
+        return plan
     for g in range(G):
         plan[(game0 + g) * ticks // G_total].append(g)
     return plan
@@ -191,6 +194,7 @@ def run_mixed(args, rank, dev):
 WORKLOAD_DESC = {
     "selfplay": "16x16 basesWorkers selfplay, random masked actions (device Philox sampler), get_action_mask+sample+step per env-step",
     "coac": "16x16 basesWorkers, every env vs device coacAI (k_bot), random masked agent actions",
+    "passive": "16x16 basesWorkers, every env vs passiveAI, random masked agent actions",
     "workerrush": "16x16 basesWorkers, every env vs device workerRushAI (k_bot), random masked agent actions",
     "partial_obs": "16x16 basesWorkers selfplay, partial_obs=True (31 planes), random masked actions",
     "8x8": "8x8 basesWorkers selfplay, random masked actions",
@@ -369,31 +373,39 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def cpu_baseline(seconds, envs=512, one_core_seconds=6.0):
+# workloads with a CPU leg (M1 selfplay, M2 vs passiveAI, M3 vs coacAI)
+CPU_WORKLOADS = ("selfplay", "passive", "coac")
+
+
+def cpu_baseline(seconds, envs=512, one_core_seconds=6.0, workload="selfplay"):
     """The oracle (C restatement, OpenMP over games) on a bounded sample of the
-    same workload: 16x16 basesWorkers selfplay, random masked actions; all host
-    cores, plus a 1-core sample in a child process (OMP_NUM_THREADS=1)."""
+    same workload (16x16 basesWorkers; selfplay, or every env vs the workload's
+    bot; random masked actions); all host cores, plus a 1-core sample in a child
+    process (OMP_NUM_THREADS=1)."""
     import subprocess
 
-    res = cpu_sample(seconds, envs)
+    res = cpu_sample(seconds, envs, workload)
     if one_core_seconds > 0:
         env = dict(os.environ, OMP_NUM_THREADS="1")
-        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-sample", str(one_core_seconds)], env=env,
-                             capture_output=True, text=True, timeout=120)
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-sample", str(one_core_seconds), workload],
+                             env=env, capture_output=True, text=True, timeout=120)
         one = json.loads(out.stdout.strip().splitlines()[-1])
         res["value_1core"] = one["value"]
         res["sample_1core"] = one["sample"]
     return res
 
 
-def cpu_sample(seconds, envs=512):
+def cpu_sample(seconds, envs=512, workload="selfplay"):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from oracle_py import OracleVecEnv
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     path = os.path.join(REPO, "microrts-py_amd", "gym_microrts", "microrts", MAP)
-    o = OracleVecEnv(envs, 0, [path], max_steps=2000)
+    _, nsp, nbot, bot, _ = WORKLOADS[workload]
+    nsp = envs if nsp == "all" else nsp
+    nbot = envs if nbot == "all" else nbot
+    o = OracleVecEnv(nsp, nbot, [path], max_steps=2000, ai2s=[bot] * nbot)
     o.reset()
     o.bench_steps(5, 1, 0)
     steps = 0
@@ -404,13 +416,14 @@ def cpu_sample(seconds, envs=512):
     dt = time.perf_counter() - t0
     o.close()
     return {"value": envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/libmrts_oracle.so ovec_bench_steps, {envs} selfplay envs x {steps} steps ({dt:.1f} s), "
-                      f"16x16 basesWorkers, masks + sampler + step + obs encode in C, OpenMP over envs, OMP_NUM_THREADS={threads}"}
+            "sample": f"oracle/libmrts_oracle.so ovec_bench_steps, {envs} {'selfplay envs' if nsp else f'envs vs {bot}'} x "
+                      f"{steps} steps ({dt:.1f} s), 16x16 basesWorkers, masks + sampler + step{' + bot' if nbot else ''} + obs "
+                      f"encode in C, OpenMP over envs, OMP_NUM_THREADS={threads}"}
 
 
 def main():
-    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-sample":   # child of cpu_baseline (no GPU use)
-        print(json.dumps(cpu_sample(float(sys.argv[2]), envs=64)), flush=True)
+    if len(sys.argv) == 4 and sys.argv[1] == "--cpu-sample":   # child of cpu_baseline (no GPU use)
+        print(json.dumps(cpu_sample(float(sys.argv[2]), envs=64, workload=sys.argv[3])), flush=True)
         return
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -506,8 +519,8 @@ def main():
             out["config"]["api"] = args.api
             out["metric"] = ("env-steps/sec, reference numpy contract (obs / masks / rewards copied to the host, host "
                              "actions in: PCIe-inclusive; not the headline)")
-        if world == 1 and not args.no_cpu_baseline and args.workload == "selfplay":
-            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+        if world == 1 and not args.no_cpu_baseline and args.workload in CPU_WORKLOADS:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, workload=args.workload)
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

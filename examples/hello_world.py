@@ -5,6 +5,11 @@ step -- with the configuration BASELINE.json states (2 selfplay envs + 2 bot env
 vs coacAI; the reference script's own `prior=True, graph_depth, graph_vector_length`
 kwargs are rejected by its vec env).
 
+Provenance: `softmax`, `sample` and the body of the loop are a near-verbatim
+adaptation of the reference's /root/reference/hello_world.py:27-67 -- the
+workload definition of configs[0] (SURVEY.md §8d names that sampler), kept as
+the reference wrote it on purpose; this file is an example, not engine code.
+
   python examples/hello_world.py [--steps N]
 """
 import argparse
@@ -32,7 +37,10 @@ def sample(logits, rng):
     return (u < c).argmax(axis=1).reshape(-1, 1)
 
 
-def main(steps=10000, seed=0, render=True):
+def main(steps=10000, seed=0, render=True, trace=None):
+    """Runs the loop; returns the number of finished episodes.  `trace` (a list)
+    receives (mask, action, obs, reward, done) of every step (tests replay it
+    through the oracle)."""
     envs = MicroRTSGridModeVecEnv(
         num_selfplay_envs=2,
         num_bot_envs=2,
@@ -66,7 +74,11 @@ def main(steps=10000, seed=0, render=True):
             ),
             axis=1,
         )
+        if trace is not None:
+            mask = np.where(action_mask == -9e8, 0, action_mask).reshape(envs.num_envs, -1, action_mask.shape[-1])
         next_obs, reward, done, info = envs.step(action)
+        if trace is not None:
+            trace.append((mask, action.reshape(envs.num_envs, -1), next_obs.copy(), reward.copy(), done.copy()))
         episodes += int(done.sum())
     envs.close()
     return episodes

@@ -76,6 +76,8 @@ typedef struct {
                                     random bots' streams so shard r's games play exactly
                                     as games [game_offset, game_offset + num_games) of
                                     one unsharded run; 0 otherwise                    */
+    int32_t map_capacity;        /* map template slots (>= num_maps; 0 -> num_maps):
+                                    room for maps added later with mrts_add_map      */
 } mrts_config;
 
 typedef struct {
@@ -154,6 +156,13 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
 /* Map cycling (vec_env.py:1038-1056): reset `count` games (host arrays) onto
  * the given map indices and rewrite their envs' obs. */
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);
+
+/* JNIGridnetVecClient.clients[i].mapPath = path / .selfPlayClients[j].mapPath =
+ * path (vec_env.py:1044, 1051): the Java client re-reads the map file at its next
+ * reset.  Here the map is loaded into a free template slot (config map_capacity)
+ * and its index returned, for mrts_reset_games; a path already in the table
+ * returns its existing index.  Same height x width as the handle's maps. */
+int mrts_add_map(mrts_vec *h, void *stream, const char *path, int32_t *index);
 
 /* Random masked action sampler of hello_world.py:27-64 on the device
  * (Philox4x32-10 keyed by seed, counter = (cell, env0 + env, step)): env0 is the

@@ -154,6 +154,8 @@ struct mrts_vec {
     int nsp = 0, nbot = 0, ngames = 0, nenvs = 0, max_steps = 0, partial_obs = 0, obs_float = 0;
     int W = 0, H = 0, HW = 0;
     std::vector<MapData> maps;
+    std::vector<std::string> map_path;   // as given to mrts_create / mrts_add_map
+    int map_capacity = 0;                // map template slots carved in the workspace
     std::vector<int32_t> game_map;
     std::vector<int32_t> bot_ai;
     std::vector<int32_t> bot_ai0;   // -1: the agent plays player 0
@@ -206,10 +208,15 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     h->max_steps = cfg->max_steps;
     h->partial_obs = cfg->partial_obs;
     h->obs_float = cfg->obs_dtype == MRTS_OBS_FLOAT32;
+    if (cfg->map_capacity != 0 && cfg->map_capacity < cfg->num_maps)
+        return fail(h, MRTS_EINVAL, "map_capacity must be 0 or >= num_maps");
+    h->map_capacity = cfg->map_capacity ? cfg->map_capacity : cfg->num_maps;
     h->maps.resize(cfg->num_maps);
     for (int i = 0; i < cfg->num_maps; i++) {
         std::string e;
-        if (!load_map(cfg->map_paths[i], &h->maps[i], &e)) return fail(h, MRTS_EIO, e);
+        if (!cfg->map_paths[i] || !load_map(cfg->map_paths[i], &h->maps[i], &e))
+            return fail(h, MRTS_EIO, cfg->map_paths[i] ? e : "null map path");
+        h->map_path.emplace_back(cfg->map_paths[i]);
         if (i > 0 && (h->maps[i].w != h->maps[0].w || h->maps[i].h != h->maps[0].h))
             return fail(h, MRTS_EINVAL, "all maps of one vec env must share height x width (vec_env.py:149-150)");
     }
@@ -252,9 +259,9 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     size_t o = 0;
     h->off_cells = o; o = align256(o + (size_t)h->ngames * h->HW * sizeof(int4));
     h->off_genv = o; o = align256(o + (size_t)h->ngames * MRTS_GENV_WORDS * sizeof(int32_t));
-    h->off_mcells = o; o = align256(o + (size_t)cfg->num_maps * h->HW * sizeof(int4));
-    h->off_mwall = o; o = align256(o + (size_t)cfg->num_maps * h->HW);
-    h->off_mscal = o; o = align256(o + (size_t)cfg->num_maps * MRTS_MAP_SCALARS * sizeof(int32_t));
+    h->off_mcells = o; o = align256(o + (size_t)h->map_capacity * h->HW * sizeof(int4));
+    h->off_mwall = o; o = align256(o + (size_t)h->map_capacity * h->HW);
+    h->off_mscal = o; o = align256(o + (size_t)h->map_capacity * MRTS_MAP_SCALARS * sizeof(int32_t));
     h->off_scratch = o; o = align256(o + (size_t)2 * h->ngames * sizeof(int32_t));
     h->off_botai = o; o = align256(o + (size_t)(h->nbot + 1) * sizeof(int32_t));
     h->off_botai0 = o; o = align256(o + (size_t)(h->nbot + 1) * sizeof(int32_t));
@@ -471,6 +478,41 @@ int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int3
     // the host staging vector must outlive the copy
     e = hipStreamSynchronize(s);
     return e ? hip_fail(h, e, "reset_games sync") : MRTS_OK;
+}
+
+int mrts_add_map(mrts_vec *h, void *stream, const char *path, int32_t *index) {
+    if (!bound(h) || !path || !index) return fail(h, MRTS_EINVAL, "add_map: not bound or null argument");
+    for (size_t i = 0; i < h->map_path.size(); i++)
+        if (h->map_path[i] == path) {
+            *index = (int32_t)i;
+            return MRTS_OK;
+        }
+    if ((int)h->maps.size() >= h->map_capacity) return fail(h, MRTS_EINVAL, "add_map: every map slot is taken (map_capacity)");
+    MapData m;
+    std::string err;
+    if (!load_map(path, &m, &err)) return fail(h, MRTS_EIO, err);
+    if (m.w != h->W || m.h != h->H)
+        return fail(h, MRTS_EINVAL, "add_map: all maps of one vec env must share height x width (vec_env.py:149-150)");
+    const int i = (int)h->maps.size();
+    int32_t scal[MRTS_MAP_SCALARS] = {0};
+    scal[MRTS_M_RES0] = m.res[0];
+    scal[MRTS_M_RES1] = m.res[1];
+    scal[MRTS_M_NUNITS] = m.nunits;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    // a slot no game uses yet: nothing in flight reads it
+    if ((e = hipMemcpyAsync(h->ws + h->off_mcells + (size_t)i * h->HW * sizeof(int4), m.cells.data(), sizeof(int4) * h->HW,
+                            hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(h->ws + h->off_mwall + (size_t)i * h->HW, m.wall.data(), h->HW, hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(h->ws + h->off_mscal + (size_t)i * MRTS_MAP_SCALARS * sizeof(int32_t), scal, sizeof(scal),
+                            hipMemcpyHostToDevice, s)) ||
+        (e = hipStreamSynchronize(s)))
+        return hip_fail(h, e, "add_map upload");
+    h->maps.push_back(std::move(m));
+    h->map_path.emplace_back(path);
+    h->base.nmaps = (int)h->maps.size();
+    *index = i;
+    return MRTS_OK;
 }
 
 int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw, int32_t env0, uint64_t seed, uint32_t step,

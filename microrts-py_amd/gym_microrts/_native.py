@@ -47,6 +47,7 @@ class Config(ctypes.Structure):
         ("obs_dtype", ctypes.c_int32),
         ("bot_ai0", ctypes.POINTER(ctypes.c_int32)),
         ("game_offset", ctypes.c_int32),
+        ("map_capacity", ctypes.c_int32),
     ]
 
 
@@ -76,6 +77,7 @@ SIGNATURES = {
     "mrts_set_reward_weight": (ctypes.c_int, [P, P, ctypes.c_int32]),
     "mrts_step_weighted": (ctypes.c_int, [P, P, P, P, P, P, P, P, P]),
     "mrts_reset_games": (ctypes.c_int, [P, P, P, P, ctypes.c_int32, P]),
+    "mrts_add_map": (ctypes.c_int, [P, P, ctypes.c_char_p, P]),
     "mrts_sample_actions": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
     "mrts_sample_actions_src": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                                ctypes.c_uint32, P]),
@@ -118,7 +120,7 @@ def check(rc, handle=None, what="call"):
 
 
 def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, game_map, bot_ai, obs_dtype, bot_ai0=None,
-           game_offset=0):
+           game_offset=0, map_capacity=0):
     cfg = Config()
     cfg.num_selfplay_envs = num_selfplay_envs
     cfg.num_bot_envs = num_bot_envs
@@ -133,6 +135,7 @@ def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, g
     cfg.bot_ai = ctypes.cast(ai, ctypes.POINTER(ctypes.c_int32))
     cfg.obs_dtype = obs_dtype
     cfg.game_offset = int(game_offset)
+    cfg.map_capacity = int(map_capacity)
     if bot_ai0 is not None:
         a0 = (ctypes.c_int32 * max(1, len(bot_ai0)))(*bot_ai0)
         cfg.bot_ai0 = ctypes.cast(a0, ctypes.POINTER(ctypes.c_int32))
@@ -145,6 +148,13 @@ def create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, map_paths, g
         cls = MicroRTSNotImplemented if rc == -4 else MicroRTSError
         raise cls(f"libmicrorts_amd create failed ({ERROR_NAMES.get(rc, rc)}): {msg}")
     return h
+
+
+def add_map(h, stream, path):
+    """mrts_add_map: the map-table index of `path`, loading it if new."""
+    idx = ctypes.c_int32(-1)
+    check(lib().mrts_add_map(h, stream, path.encode(), ctypes.byref(idx)), h, "add_map")
+    return int(idx.value)
 
 
 def info(h):

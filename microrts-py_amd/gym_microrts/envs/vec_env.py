@@ -84,6 +84,50 @@ class LazyInfos:
             yield {"raw_rewards": r}
 
 
+class HostArrayPool:
+    """Page-locked host arrays handed out as fresh numpy arrays.
+
+    The reference's numpy contract returns a new array from every call
+    (`np.array(...)` of the JPype result, vec_env.py:280, 1003, 1097), and a
+    caller may keep it as long as it likes.  Copying the device outputs into
+    fresh pageable arrays costs a staged D2H plus first-touch page faults on
+    every call (hundreds of MB per step at 8192 envs).  This pool keeps a few
+    page-locked buffers per output and hands out a numpy view of one; a buffer
+    is reused only when no array derived from it is still alive (every numpy
+    view, and torch.from_numpy of one, keeps the owning array referenced), so a
+    returned array is never overwritten behind the caller's back.  When every
+    buffer is held, the pool grows up to `limit`, then falls back to plain
+    fresh arrays."""
+
+    def __init__(self, pinned=True, limit=3):
+        import sys
+
+        self._refs = sys.getrefcount
+        self.pinned = pinned
+        self.limit = limit
+        self._bufs = {}   # key -> [(tensor, owner ndarray, idle refcount)]
+
+    def d2h(self, key, src):
+        """Enqueue src (device tensor) -> a free host buffer on the current stream;
+        the returned numpy array is valid after the stream is synchronised."""
+        bufs = self._bufs.setdefault(key, [])
+        for t, n, idle in bufs:
+            if self._refs(n) == idle and t.shape == src.shape and t.dtype == src.dtype:
+                t.copy_(src, non_blocking=True)
+                return n[...]
+        if len(bufs) < self.limit:
+            t = torch.empty(tuple(src.shape), dtype=src.dtype, pin_memory=self.pinned)
+            n = t.numpy()
+            entry = [t, n, 0]
+            bufs.append(entry)
+            entry[2] = self._refs(n)   # the pool's slot + this frame's name + the call (as in the loop above)
+            t.copy_(src, non_blocking=True)
+            return n[...]
+        out = torch.empty(tuple(src.shape), dtype=src.dtype)
+        out.copy_(src)
+        return out.numpy()
+
+
 class MicroRTSGridModeVecEnv:
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 150}
     _cycle_min = 0   # map cycling when len(cycle_maps) > _cycle_min (vec_env.py:1038)
@@ -255,6 +299,8 @@ class MicroRTSGridModeVecEnv:
         self.source_unit_idxs = np.tile(np.arange(self.height * self.width), (self.num_envs, 1))
         self.source_unit_idxs = self.source_unit_idxs.reshape((self.source_unit_idxs.shape + (1,)))
         self._mask_fresh = False   # _mask / _src hold getMasks(0) of the current state
+        self._pool = None          # numpy contract: page-locked output arrays (HostArrayPool)
+        self._act_stage = None     # numpy contract: page-locked int64 staging of the host actions
         # optional {kernel name: [(start, end) torch.cuda.Event]} filled around
         # each engine launch on the launch stream (bench.py roofline timing)
         self.kernel_events = None
@@ -289,10 +335,22 @@ class MicroRTSGridModeVecEnv:
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    def _host(self, key, t):
+        """numpy contract: a fresh host array of device tensor t (HostArrayPool),
+        enqueued on the current stream; valid after _sync()."""
+        if self._pool is None:
+            self._pool = HostArrayPool(pinned=self.device.type == "cuda")
+        return self._pool.d2h(key, t)
+
+    def _sync(self):
+        torch.cuda.current_stream(self.device).synchronize()
+
     def _obs_out(self):
         if self.return_tensors:
             return self._obs
-        return self._obs.cpu().numpy()
+        obs = self._host("obs", self._obs)
+        self._sync()
+        return obs
 
     # ------------------------------------------------------------------- API
     def reset(self):
@@ -310,7 +368,9 @@ class MicroRTSGridModeVecEnv:
             self._mask_fresh = True
         if self.return_tensors:
             return self._mask
-        return self._mask.cpu().numpy()
+        mask = self._host("mask", self._mask)
+        self._sync()
+        return mask
 
     @property
     def source_unit_mask(self):
@@ -327,7 +387,12 @@ class MicroRTSGridModeVecEnv:
             self._actions.copy_(a)
         else:
             a = np.asarray(actions).reshape(self.num_envs, hw, 7)
-            self._actions.copy_(torch.from_numpy(np.ascontiguousarray(a.astype(np.int64, copy=False))))
+            if self._act_stage is None:
+                self._act_stage = torch.empty(tuple(self._actions.shape), dtype=torch.int64, pin_memory=True)
+            # one host pass into page-locked memory, then a DMA at full PCIe rate (a
+            # pageable source would be staged by the runtime in small chunks)
+            np.copyto(self._act_stage.numpy(), a, casting="unsafe")
+            self._actions.copy_(self._act_stage, non_blocking=True)
         self._actions_in = self._actions
 
     def step_wait(self):
@@ -352,13 +417,19 @@ class MicroRTSGridModeVecEnv:
             return self._obs, self._rew, self._done0, LazyInfos(raw)
         self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
                      self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
-        reward = self._raw.cpu().numpy()
-        done = self._done.cpu().numpy().astype(bool)
+        reward = self._host("raw", self._raw)
+        done = self._host("done", self._done)
+        cycling = len(self.cycle_maps) > self._cycle_min
+        if not cycling:   # one stream sync for every output
+            obs = self._host("obs", self._obs)
+        self._sync()
+        done = done.astype(bool)
         if not self.reward_shaping:
             reward[:, 1:] = 0
-        if len(self.cycle_maps) > self._cycle_min:
+        if cycling:
             self._cycle(done[:, 0])
-        obs = self._obs.cpu().numpy()
+            obs = self._host("obs", self._obs)
+            self._sync()
         infos = [{"raw_rewards": item} for item in reward]
         return obs, reward @ self.reward_weight, done[:, 0], infos
 

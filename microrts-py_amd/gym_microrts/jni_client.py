@@ -15,6 +15,10 @@ back from device buffers, exactly as JPype copied them out of the JVM.
   .gameStep(actions, players)-> Response   (actions: per env a [k_i][8] array of (cell, 7 components) rows)
   .getMasks(player)          -> int32 [N][H][W][79]
   .close()
+  .clients[j]                -> bot env j's game client (JNIGridnetClient): .mapPath, .reset(p), .getResponse(p)
+  .selfPlayClients[k]        -> selfplay game k (JNIGridnetClientSelfPlay, envs 2k / 2k+1): .mapPath, .reset(),
+                                .getResponse(p)
+  .render(True) / .sendUTT() on either kind (the reference's render_client, vec_env.py:272-276, 1077-1083)
 """
 import ctypes
 import os
@@ -32,6 +36,61 @@ class Response:
         self.observation = observation
         self.reward = reward
         self.done = done
+
+
+RENDER_SIZE = 640   # PhysicalGameStatePanel frame of the reference (vec_env.py:1083)
+MAP_SLOTS = 64      # map-table slots for maps set later through .mapPath
+
+
+class GameClient:
+    """One game of the vec client: ts.JNIGridnetClient (a bot env, `envs` = [env])
+    or ts.JNIGridnetClientSelfPlay (`envs` = [2k, 2k + 1]).  The calls the
+    reference's map cycling and render make (vec_env.py:272-276, 1044-1054,
+    1077-1083):
+
+      c.mapPath = path       the map of the game's next reset (Java re-reads the
+                             file; here mrts_add_map loads it into a free slot)
+      c.reset(p=0)           the game back to mapPath (mrts_reset_games); a bot
+                             client returns player p's Response, a selfplay one
+                             nothing (then getResponse(0) / getResponse(1))
+      c.getResponse(p)       Response of the game's player p: raw observation of
+                             this state, reward and done of the last step (zero after a reset)
+      c.render(True)         the frame as BGR bytes [640*640*3] (the reference turns
+                             them into an image and flips them back to RGB); render(False)
+                             opens no window on a headless GPU host and returns None
+      c.sendUTT()            UnitTypeTable JSON
+    """
+
+    def __init__(self, vec, game, envs, map_path):
+        self._vec = vec
+        self.game = game
+        self.envs = envs
+        self._map_path = map_path
+
+    @property
+    def mapPath(self):  # noqa: N802 (Java name)
+        return self._map_path
+
+    @mapPath.setter
+    def mapPath(self, path):  # noqa: N802
+        self._vec._map_id(path)   # load now: a bad path fails at the assignment
+        self._map_path = path
+
+    def reset(self, player=None):
+        self._vec._reset_game(self.game, self._vec._map_id(self._map_path))
+        if len(self.envs) == 1:
+            return self.getResponse(0 if player is None else player)
+        return None
+
+    def getResponse(self, player):  # noqa: N802
+        env = self.envs[player] if len(self.envs) > 1 else self.envs[0]
+        return self._vec._env_response(env)
+
+    def render(self, rgb):
+        return self._vec._render(self.envs[0], rgb)
+
+    def sendUTT(self):  # noqa: N802
+        return self._vec.utt_json
 
 
 class JNIGridnetVecClient:
@@ -59,7 +118,9 @@ class JNIGridnetVecClient:
                 raise _native.MicroRTSNotImplemented(f"bot {d} has no device implementation")
             bot_ai.append(d.ai_id)
         self._h = _native.create(num_selfplay_envs, num_bot_envs, max_steps, partial_obs, table, game_map, bot_ai,
-                                 _native.MRTS_OBS_INT32)
+                                 _native.MRTS_OBS_INT32, map_capacity=len(table) + MAP_SLOTS)
+        self.microrts_path = microrts_path
+        self._map_table = list(table)
         info = _native.info(self._h)
         self.height, self.width, self.P_raw = info.height, info.width, 7 if partial_obs else 6
         hw = self.height * self.width
@@ -74,6 +135,12 @@ class JNIGridnetVecClient:
             self._done = torch.zeros((n, 6), dtype=torch.uint8, device=self.device)
         L = _native.lib()
         _native.check(L.mrts_bind_workspace(self._h, self._ws.data_ptr(), self._stream()), self._h, "bind_workspace")
+        self.utt_json = L.mrts_utt_json(self._h).decode()
+        # per-game clients (Java: JNIGridnetClientSelfPlay per pair, JNIGridnetClient per bot env)
+        self.selfPlayClients = [GameClient(self, k, [2 * k, 2 * k + 1], table[game_map[k]]) for k in range(nsp_games)]
+        self.clients = [GameClient(self, nsp_games + j, [num_selfplay_envs + j], table[game_map[nsp_games + j]])
+                        for j in range(num_bot_envs)]
+        self._frame = None
 
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -109,6 +176,34 @@ class JNIGridnetVecClient:
         _native.check(_native.lib().mrts_step(self._h, self._stream(), a.data_ptr(), s.data_ptr(), self._obs.data_ptr(),
                                               self._rew.data_ptr(), self._done.data_ptr()), self._h, "step")
         return self._response()
+
+    # ---- per-game calls (GameClient)
+    def _map_id(self, path):
+        full = path if os.path.isabs(path) else os.path.join(self.microrts_path, path)
+        return _native.add_map(self._h, self._stream(), full)
+
+    def _reset_game(self, game, map_id):
+        g = (ctypes.c_int32 * 1)(game)
+        m = (ctypes.c_int32 * 1)(map_id)
+        _native.check(_native.lib().mrts_reset_games(self._h, self._stream(), g, m, 1, self._obs.data_ptr()), self._h,
+                      "reset_games")
+        envs = [e for c in self.selfPlayClients + self.clients if c.game == game for e in c.envs]
+        self._rew[envs] = 0
+        self._done[envs] = 0
+
+    def _env_response(self, env):
+        _native.check(_native.lib().mrts_get_raw_obs(self._h, self._stream(), self._raw_obs.data_ptr()), self._h, "raw_obs")
+        return Response(self._raw_obs[env].cpu().numpy(), self._rew[env].cpu().numpy(),
+                        self._done[env].cpu().numpy().astype(bool))
+
+    def _render(self, env, rgb):
+        if not rgb:
+            return None   # render(False): the Swing window; no display on the GPU host
+        if self._frame is None:
+            self._frame = torch.empty((RENDER_SIZE, RENDER_SIZE, 3), dtype=torch.uint8, device=self.device)
+        _native.check(_native.lib().mrts_render(self._h, self._stream(), env, self._frame.data_ptr(), RENDER_SIZE), self._h,
+                      "render")
+        return self._frame.flip(-1).contiguous().cpu().numpy().reshape(-1)   # BGR byte order, as the Java returns
 
     def close(self):
         if getattr(self, "_h", None):

@@ -828,13 +828,13 @@ void ovec_reset_game(OVec *v, int game, int map_id) {
 }
 
 void ovec_reset(OVec *v) {
-#pragma omp parallel for schedule(dynamic, 64)
+#pragma omp parallel for schedule(dynamic, 8)
     for (int g = 0; g < v->ngames; g++) ovec_reset_game(v, g, v->game_map[g]);
 }
 
 void ovec_get_masks(OVec *v, int32_t *masks) {
     size_t stride = (size_t)v->W * v->H * 79;
-#pragma omp parallel for schedule(dynamic, 64)
+#pragma omp parallel for schedule(dynamic, 8)
     for (int g = 0; g < v->ngames; g++) {
         int e0, nv;
         env_views(v, g, &e0, &nv);
@@ -844,7 +844,7 @@ void ovec_get_masks(OVec *v, int32_t *masks) {
 
 void ovec_step(OVec *v, const int64_t *actions, const int32_t *src, double *reward, uint8_t *done) {
     int HW = v->W * v->H;
-#pragma omp parallel for schedule(dynamic, 64)
+#pragma omp parallel for schedule(dynamic, 8)
     for (int gi = 0; gi < v->ngames; gi++) {
         OGS *g = &v->gs[gi];
         int e0, nv;

@@ -64,13 +64,30 @@ def test_human_mode_warns_once_and_draws_nothing():
 
 def test_hello_world_example_runs():
     """BASELINE configs[0]: examples/hello_world.py (the reference loop, render()
-    every step) against device coacAI."""
+    every step, 2 selfplay + 2 envs vs device coacAI), its whole trajectory
+    replayed through the oracle: masks, obs, weighted rewards and dones equal at
+    every step, with the actions the script's host sampler drew."""
     import importlib.util
 
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "hello_world.py")
     spec = importlib.util.spec_from_file_location("hello_world_example", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    trace = []
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        assert mod.main(steps=300) >= 0
+        episodes = mod.main(steps=300, trace=trace)
+    assert episodes >= 0 and len(trace) == 300
+    from oracle_py import OracleVecEnv
+
+    m = "maps/16x16/basesWorkers16x16.xml"
+    o = OracleVecEnv(2, 2, [os.path.join(MAPS, m)], max_steps=2000, ai2s=["coacAI", "coacAI"],
+                     reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]))
+    o.reset()
+    for s, (mask, action, obs, reward, done) in enumerate(trace):
+        np.testing.assert_array_equal(mask, o.get_action_mask(), err_msg=f"mask at step {s}")
+        oo, ro, do, _ = o.step(action)
+        np.testing.assert_array_equal(obs, oo, err_msg=f"obs at step {s}")
+        np.testing.assert_array_equal(reward, ro)
+        np.testing.assert_array_equal(done, do)
+    o.close()
