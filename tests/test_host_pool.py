@@ -1,0 +1,42 @@
+"""HostArrayPool (the numpy contract's host outputs): an array handed out is never
+overwritten while anything derived from it is alive -- the fresh-array semantics
+of the reference's np.array(...) copies (vec_env.py:280, 1003, 1097) -- and a
+released buffer is reused.  CPU only (pinned=False, CPU source tensors)."""
+import numpy as np
+import torch
+
+from gym_microrts.envs.vec_env import HostArrayPool
+
+
+def test_live_arrays_are_never_overwritten():
+    pool = HostArrayPool(pinned=False, limit=3)
+    src = torch.arange(12, dtype=torch.int32).reshape(3, 4)
+    a = pool.d2h("obs", src)
+    np.testing.assert_array_equal(a, src.numpy())
+    held = [a.reshape(-1)[2:], torch.from_numpy(a[1])]   # derived views keep `a`'s buffer busy
+    del a
+    b = pool.d2h("obs", src + 100)
+    assert not np.shares_memory(b, held[0])
+    np.testing.assert_array_equal(held[0], np.arange(2, 12))
+    np.testing.assert_array_equal(held[1].numpy(), [4, 5, 6, 7])
+    c = pool.d2h("obs", src + 200)
+    d = pool.d2h("obs", src + 300)   # every buffer held: a plain fresh array
+    for x, k in ((b, 100), (c, 200), (d, 300)):
+        np.testing.assert_array_equal(x, src.numpy() + k)
+    assert len(pool._bufs["obs"]) == 3
+
+
+def test_released_buffer_is_reused():
+    pool = HostArrayPool(pinned=False, limit=2)
+    src = torch.ones((5, 7), dtype=torch.float64)
+    a = pool.d2h("raw", src)
+    ptr = a.ctypes.data
+    a[:, 1:] = 0   # the caller owns it (reward[:, 1:] = 0, vec_env.py:1005)
+    del a
+    b = pool.d2h("raw", src * 3)
+    assert b.ctypes.data == ptr
+    np.testing.assert_array_equal(b, np.full((5, 7), 3.0))
+    assert len(pool._bufs["raw"]) == 1
+    # a different shape under the same key gets its own buffer
+    e = pool.d2h("raw", torch.zeros((2, 2), dtype=torch.float64))
+    assert e.shape == (2, 2) and e.ctypes.data != ptr
