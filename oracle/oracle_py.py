@@ -16,7 +16,8 @@ import xml.etree.ElementTree as ET
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmrts_oracle.so")
+# MRTS_ORACLE_LIB: another build of the same sources (the ASan/UBSan one, tests/test_oracle_asan.py)
+LIB_PATH = os.environ.get("MRTS_ORACLE_LIB") or os.path.join(HERE, "libmrts_oracle.so")
 UNIT_TYPES = ["Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"]
 AI_IDS = {"passiveAI": 0, "workerRushAI": 1, "lightRushAI": 2, "randomBiasedAI": 3, "coacAI": 4,
           "POWorkerRush": 5, "POLightRush": 6, "POHeavyRush": 7, "PORangedRush": 8, "randomAI": 9}
