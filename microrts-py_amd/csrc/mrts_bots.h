@@ -119,7 +119,10 @@ struct URef {
     uint32_t u;     // unit word
 };
 
-__device__ __forceinline__ bool lane0() { return threadIdx.x == 0; }
+// lane of the bot's wavefront: k_bot is one wave; in the fused k_step any wave
+// of the workgroup may run the bot (the launch rotates it over the SIMDs)
+__device__ __forceinline__ int blane() { return (int)(threadIdx.x & 63u); }
+__device__ __forceinline__ bool lane0() { return blane() == 0; }
 __device__ __forceinline__ int iabs(int a) { return a < 0 ? -a : a; }
 
 __device__ __forceinline__ bool in_map(const BS& S, int x, int y) { return x >= 0 && y >= 0 && x < S.W && y < S.H; }
@@ -164,7 +167,7 @@ __device__ __forceinline__ int cell_of_uid(const BS& S, const BL& L, int uid, ui
         return lane_value(S.kcell, __builtin_ctzll(m));
     }
     for (int base = 0; base < S.n; base += BT) {
-        const int k = base + threadIdx.x;
+        const int k = base + blane();
         const unsigned long long m = __ballot(k < S.n && L.uuid[k] == uid);
         if (m) {
             const int c = L.ucell[base + __builtin_ctzll(m)];
@@ -217,7 +220,7 @@ __device__ __forceinline__ int closest_unit(const BS& S, const BL& L, int x, int
 template <typename F>
 __device__ __forceinline__ int closest_index(const BS& S, const BL& L, int x, int y, F want, int* dist) {
     uint32_t key = 0xFFFFFFFFu;
-    for (int k = threadIdx.x; k < S.n; k += BT) {
+    for (int k = blane(); k < S.n; k += BT) {
         int c;
         uint32_t u, a;
         list_entry(S, L, k, c, u, a);
@@ -236,7 +239,7 @@ __device__ __forceinline__ int closest_index(const BS& S, const BL& L, int x, in
 template <typename P, typename F>
 __device__ __forceinline__ void for_each_unit(const BS& S, const BL& L, P want, F body) {
     for (int base = 0; base < S.n; base += BT) {
-        const int k = base + threadIdx.x;
+        const int k = base + blane();
         int c;
         uint32_t u, a;
         list_entry(S, L, k, c, u, a);
@@ -253,7 +256,7 @@ template <typename F>
 __device__ __forceinline__ int count_where(const BS& S, const BL& L, F want) {
     int n = 0;
     for (int base = 0; base < S.n; base += BT) {
-        const int k = base + threadIdx.x;
+        const int k = base + blane();
         int c;
         uint32_t u, a;
         list_entry(S, L, k, c, u, a);
@@ -265,7 +268,7 @@ __device__ __forceinline__ int count_where(const BS& S, const BL& L, F want) {
 template <typename F>
 __device__ __forceinline__ int nth_index(const BS& S, const BL& L, int idx, F want) {
     for (int base = 0; base < S.n; base += BT) {
-        const int k = base + threadIdx.x;
+        const int k = base + blane();
         int c;
         uint32_t u, a;
         list_entry(S, L, k, c, u, a);
@@ -332,7 +335,7 @@ __device__ __forceinline__ void pa_add(BS& S, const BL& L, int c, int code) {
     S.npa++;
     S.pa_res[0] += r.res[0];
     S.pa_res[1] += r.res[1];
-    if (r.pos != -0x7fffffff && r.pos >= 0 && r.pos < S.HW && (int)threadIdx.x == r.pos / S.W)
+    if (r.pos != -0x7fffffff && r.pos >= 0 && r.pos < S.HW && blane() == r.pos / S.W)
         S.rurow |= 1u << (r.pos % S.W);
 }
 
@@ -341,7 +344,7 @@ __device__ __forceinline__ void pa_add(BS& S, const BL& L, int c, int code) {
 // the target) over free cells; the first layer that touches a free neighbour
 // of the start decides the move, ties UP, RIGHT, DOWN, LEFT.  -1 = null.
 __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
-    const int lane = threadIdx.x, sx = sc % S.W, sy = sc / S.W, r2 = range * range;
+    const int lane = blane(), sx = sc % S.W, sy = sc / S.W, r2 = range * range;
     if ((sx - tx) * (sx - tx) + (sy - ty) * (sy - ty) <= r2) return -1;
     const uint32_t rowmask = S.W == 32 ? 0xFFFFFFFFu : ((1u << S.W) - 1u);
     uint32_t fr = 0, goal = 0;
@@ -388,11 +391,11 @@ __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int r
 // and lookups are one ballot / lane read.
 __device__ __forceinline__ int find_aa(const BS& S, const BL& L, int uid) {   // first entry of the unit, lane-parallel
     if (S.naa <= BT) {
-        const unsigned long long m = __ballot((int)threadIdx.x < S.naa && S.kA.x == uid);
+        const unsigned long long m = __ballot(blane() < S.naa && S.kA.x == uid);
         return m ? __builtin_ctzll(m) : -1;
     }
     for (int base = 0; base < S.naa; base += BT) {
-        const int k = base + threadIdx.x;
+        const int k = base + blane();
         const unsigned long long m = __ballot(k < S.naa && L.aa[2 * k].x == uid);
         if (m) return base + __builtin_ctzll(m);
     }
@@ -419,7 +422,7 @@ __device__ __forceinline__ void aa_put(BS& S, const BL& L, int4 a, int4 b) {   /
         }
         k = S.naa++;
     }
-    if ((int)threadIdx.x == k) {
+    if (blane() == k) {
         S.kA = a;
         S.kB = b;
     }
@@ -601,7 +604,7 @@ __device__ __forceinline__ void melee_behavior(BS& S, const BL& L, const URef& w
     const int ux = w.c % S.W, uy = w.c / S.W;
     // first minimum in row-major scan order = min over (d^2 << 16 | cell); d^2 <= 32^2 + 64^2
     uint32_t key = 0xFFFFFFFFu;
-    for (int c = threadIdx.x; c < S.HW; c += BT) {
+    for (int c = blane(); c < S.HW; c += BT) {
         if (bit_at(L.vis, c)) continue;
         const int x = c % S.W, y = c / S.W;
         const uint32_t kk = ((uint32_t)((ux - x) * (ux - x) + (uy - y) * (uy - y)) << 16) | (uint32_t)c;
@@ -813,7 +816,7 @@ __device__ __forceinline__ int lane_closest(const BS& S, unsigned long long cand
 
 // army: 0 = coacAI (its own worker / army rules), else the rush's army unit type
 __device__ __forceinline__ void behaviours_parallel(BS& S, const BL& L, int army, bool po, bool coac) {
-    const int lane = threadIdx.x, p = S.player, res = p ? S.res[1] : S.res[0];
+    const int lane = blane(), p = S.player, res = p ? S.res[1] : S.res[0];
     const bool valid = lane < S.n;
     const uint32_t u = S.kunit;
     const int t = u_type(u), ow = u_owner(u);
@@ -1052,7 +1055,7 @@ __device__ __forceinline__ void random_biased_get_action(BS& S, const BL& L) {
     S.pa_res[0] = S.pend_res[0];
     S.pa_res[1] = S.pend_res[1];
     const int posw = (S.HW + 2 * S.W) / 32 + 1;
-    for (int i = threadIdx.x; i < posw; i += BT) L.pab[i] = L.pend[i];
+    for (int i = blane(); i < posw; i += BT) L.pab[i] = L.pend[i];
     for_each_unit(S, L, [&](int, uint32_t u, uint32_t a) { return u_owner(u) == S.player && a == 0; }, [&](const URef& ur) {
         const int c = ur.c;
         int total = 0;
@@ -1085,7 +1088,7 @@ __device__ __forceinline__ void random_single_get_action(BS& S, const BL& L) {
     S.pa_res[0] = S.pend_res[0];
     S.pa_res[1] = S.pend_res[1];
     const int posw = (S.HW + 2 * S.W) / 32 + 1;
-    for (int i = threadIdx.x; i < posw; i += BT) L.pab[i] = L.pend[i];
+    for (int i = blane(); i < posw; i += BT) L.pab[i] = L.pend[i];
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     uint32_t ctr[4] = {0xFFFFFFFFu, S.tick, (uint32_t)S.game, 0x52534E47u + (uint32_t)(1 - S.player)};
     philox_b(ctr, 0x5EED5EEDu, 0xB0B0B0B0u);
@@ -1118,7 +1121,7 @@ __device__ __forceinline__ void bot_sync() {
 
 
 // ---- the kernel ------------------------------------------------------------------------
-// ai.getAction(player, gs) of bot game b, by ONE wavefront (lanes = threadIdx.x
+// ai.getAction(player, gs) of bot game b, by ONE wavefront (lanes = blane()
 // 0..63), LDS at `smem` (bot_lds_bytes).  FUSED: run by wave 0 of a k_step
 // workgroup for the NEXT tick while the other waves stream the outputs (no
 // workgroup barriers here then; the game state was stored before the caller's
@@ -1134,7 +1137,7 @@ template <bool FUSED>
 __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem,
                                          const int32_t* step_sc = nullptr, bool pre_ok = false, int4 pre_aa = int4{0, 0, 0, 0},
                                          int4 pre_aa2 = int4{0, 0, 0, 0}) {
-    const int g = p.nsp_games + b, lane = threadIdx.x;
+    const int g = p.nsp_games + b, lane = blane();
     const int HW = p.HW, W = p.W;
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
     const int w_aa = player ? MRTS_G_AA_N : MRTS_G_AA_N0, w_npa = player ? MRTS_G_NPA : MRTS_G_NPA0;
