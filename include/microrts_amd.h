@@ -154,8 +154,17 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
                        double *raw_reward, uint8_t *done, double *reward, uint8_t *done0);
 
 /* Map cycling (vec_env.py:1038-1056): reset `count` games (host arrays) onto
- * the given map indices and rewrite their envs' obs. */
+ * the given map indices and rewrite their envs' obs; parked games play again. */
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);
+
+/* Park `count` games (host array): they stop ticking -- mrts_step, mrts_get_masks
+ * and the bots skip them -- and their envs' obs (and bound mask / source) rows
+ * are written as zeros now; reward / done rows are left to the caller.
+ * mrts_reset_games restarts a parked game on a map (mrts_reset keeps it parked
+ * and writes its zeros again).  Map cycling across map sizes
+ * (MicroRTSSizeCyclingVecEnv): a game lives in one engine per size and plays in
+ * one of them. */
+int mrts_park_games(mrts_vec *h, void *stream, const int32_t *games, int32_t count, void *obs);
 
 /* JNIGridnetVecClient.clients[i].mapPath = path / .selfPlayClients[j].mapPath =
  * path (vec_env.py:1044, 1051): the Java client re-reads the map file at its next

@@ -22,6 +22,7 @@ __global__ __launch_bounds__(BT) void k_bot(EngineParams p) {
         b = p.bot_games[blockIdx.x] - p.nsp_games;
         if (b < 0) return;   // a selfplay game
     }
+    if (game_parked(p, p.nsp_games + b)) return;
     bot_game<false>(p, b, player, smem);
 }
 

@@ -163,7 +163,8 @@ struct mrts_vec {
     int game_offset = 0;
     // workspace carving
     size_t off_cells = 0, off_genv = 0, off_mcells = 0, off_mwall = 0, off_mscal = 0, off_scratch = 0, total = 0;
-    size_t off_botai = 0, off_botai0 = 0, off_aa = 0, off_botpa = 0;
+    size_t off_botai = 0, off_botai0 = 0, off_aa = 0, off_botpa = 0, off_parked = 0;
+    std::vector<uint8_t> parked;   // host mirror of the device parked flags (mrts_park_games)
     int nbot_active = 0;
     unsigned char *ws = nullptr;
     std::vector<int32_t> scratch_host;
@@ -267,6 +268,7 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     h->off_botai0 = o; o = align256(o + (size_t)(h->nbot + 1) * sizeof(int32_t));
     h->off_aa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * 2 * h->HW * 2 * sizeof(int4) : 0));
     h->off_botpa = o; o = align256(o + (h->nbot_active ? (size_t)h->nbot * 2 * h->HW * sizeof(int32_t) : 0));
+    h->off_parked = o; o = align256(o + (size_t)h->ngames);
     h->total = o;
     h->err.clear();
     return MRTS_OK;
@@ -336,8 +338,19 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.botpa = h->nbot_active ? (int32_t *)(h->ws + h->off_botpa) : nullptr;
     p.nbot_active = h->nbot_active;
     p.game_offset = h->game_offset;
+    p.parked = nullptr;   // until a game is parked
+    h->parked.assign(h->ngames, 0);
     h->err.clear();
     return MRTS_OK;
+}
+
+// host flags -> device; the engine checks them from now on
+static hipError_t upload_parked(mrts_vec *h, hipStream_t s) {
+    uint8_t *d = h->ws + h->off_parked;
+    hipError_t e = hipMemcpyAsync(d, h->parked.data(), h->parked.size(), hipMemcpyHostToDevice, s);
+    if (!e) e = hipStreamSynchronize(s);   // the host vector may change before the copy would run
+    if (!e) h->base.parked = d;
+    return e;
 }
 
 static bool bound(mrts_vec *h) { return h && h->ws; }
@@ -463,6 +476,17 @@ int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int3
         h->game_map[games[i]] = maps[i];
     }
     hipStream_t s = (hipStream_t)stream;
+    if (h->base.parked) {   // the listed games play again
+        bool any = false;
+        for (int i = 0; i < count; i++) {
+            any |= h->parked[games[i]] != 0;
+            h->parked[games[i]] = 0;
+        }
+        if (any) {
+            hipError_t e = upload_parked(h, s);
+            if (e) return hip_fail(h, e, "reset_games unpark");
+        }
+    }
     h->scratch_host.assign(games, games + count);
     h->scratch_host.insert(h->scratch_host.end(), maps, maps + count);
     int32_t *dg = (int32_t *)(h->ws + h->off_scratch);
@@ -513,6 +537,32 @@ int mrts_add_map(mrts_vec *h, void *stream, const char *path, int32_t *index) {
     h->base.nmaps = (int)h->maps.size();
     *index = i;
     return MRTS_OK;
+}
+
+int mrts_park_games(mrts_vec *h, void *stream, const int32_t *games, int32_t count, void *obs) {
+    if (!bound(h) || !obs || count < 0 || count > h->ngames || (count && !games))
+        return fail(h, MRTS_EINVAL, "park_games: bad arguments");
+    if (count == 0) return MRTS_OK;
+    for (int i = 0; i < count; i++) {
+        if (games[i] < 0 || games[i] >= h->ngames) return fail(h, MRTS_EINVAL, "park_games: game out of range");
+        h->parked[games[i]] = 1;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = upload_parked(h, s);
+    if (e) return hip_fail(h, e, "park_games upload");
+    // k_reset over the list: parked games write zero obs / masks / sources
+    h->scratch_host.assign(games, games + count);
+    h->scratch_host.insert(h->scratch_host.end(), games, games + count);   // (map list unused for parked games)
+    int32_t *dg = (int32_t *)(h->ws + h->off_scratch);
+    if ((e = hipMemcpyAsync(dg, h->scratch_host.data(), sizeof(int32_t) * 2 * count, hipMemcpyHostToDevice, s)))
+        return hip_fail(h, e, "park_games upload");
+    EngineParams p = h->base;
+    p.obs = obs;
+    p.mask = h->next_mask;
+    p.src_out = h->next_src;
+    e = mrts_engine_reset(&p, s, dg, dg + count, count);
+    if (!e) e = hipStreamSynchronize(s);
+    return e ? hip_fail(h, e, "park_games launch") : MRTS_OK;
 }
 
 int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw, int32_t env0, uint64_t seed, uint32_t step,

@@ -37,7 +37,10 @@ struct EngineParams {
     int bot_ngames;
     int fuse_bots;          // k_step: wave 0 of each bot game's workgroup decides the next tick's bot actions
     int game_offset;        // global index of game 0 (a shard of a larger batch): keys the bots' RNG
+    const uint8_t *parked;  // [G] 1 = parked (mrts_park_games): no tick, no masks / bots, zero outputs at
+                            // reset; null while no game was ever parked
 };
+__device__ __forceinline__ bool game_parked(const EngineParams &p, int g) { return p.parked && p.parked[g]; }
 
 extern "C" {
 hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t *games, const int32_t *maps, int count);

@@ -332,13 +332,31 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     }
 }
 
+// A parked game's envs read zero: obs rows, and (bound) mask / source rows.
+template <int NT, int P, typename OT>
+__device__ __forceinline__ void zero_outputs(const EngineParams& p, const Game& G) {
+    const size_t n = (size_t)G.nviews * p.HW;
+    OT* obs = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * p.HW * P;
+    for (size_t i = threadIdx.x; i < n * P; i += NT) obs[i] = (OT)0;
+    if (p.mask) {
+        int32_t* m = p.mask + (size_t)G.env0 * p.HW * MRTS_MASK_CH;
+        for (size_t i = threadIdx.x; i < n * MRTS_MASK_CH; i += NT) m[i] = 0;
+        for (size_t i = threadIdx.x; i < n; i += NT) p.src_out[(size_t)G.env0 * p.HW + i] = 0;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Reset kernel: every game (or the listed ones) back to its map; obs out.
+// Parked games (mrts_park_games) keep their state and write zero outputs.
 template <int NT, int P, typename OT>
 __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* games, const int32_t* maps, int count) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds L = carve(smem, p.HW, p.W, NT);
     int g = games ? games[blockIdx.x] : blockIdx.x;
+    if (game_parked(p, g)) {
+        zero_outputs<NT, P, OT>(p, game_of(p, g));
+        return;
+    }
     int map = maps ? maps[blockIdx.x] : p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
     // a reset keeps the never-reset counters (bot RNG ticks, rollout statistics)
     if (threadIdx.x < SC_WORDS) {
@@ -364,6 +382,7 @@ __global__ __launch_bounds__(NT) void k_raw(EngineParams p, int32_t* raw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds L = carve(smem, p.HW, p.W, NT);
     const int g = blockIdx.x, HW = p.HW;
+    if (game_parked(p, g)) return;
     load_game<NT>(p, L, g);
     const Game G = game_of(p, g);
     const int PR = p.partial_obs ? 7 : 6, nw = HW / 32 + 1;
@@ -392,6 +411,7 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds L = carve(smem, p.HW, p.W, NT);
     const int g = blockIdx.x;
+    if (game_parked(p, g)) return;   // its rows were zeroed when it was parked
     load_game<NT>(p, L, g);
     emit_outputs<NT, 29, int32_t>(p, L, game_of(p, g), false, true);
 }
@@ -684,6 +704,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
     const int g = blockIdx.x;
+    if (game_parked(p, g)) return;   // no tick: its outputs stay zero (mrts_park_games)
     if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
     const Game G = game_of(p, g);
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;

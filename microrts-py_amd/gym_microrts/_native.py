@@ -78,6 +78,7 @@ SIGNATURES = {
     "mrts_step_weighted": (ctypes.c_int, [P, P, P, P, P, P, P, P, P]),
     "mrts_reset_games": (ctypes.c_int, [P, P, P, P, ctypes.c_int32, P]),
     "mrts_add_map": (ctypes.c_int, [P, P, ctypes.c_char_p, P]),
+    "mrts_park_games": (ctypes.c_int, [P, P, P, ctypes.c_int32, P]),
     "mrts_sample_actions": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
     "mrts_sample_actions_src": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                                ctypes.c_uint32, P]),

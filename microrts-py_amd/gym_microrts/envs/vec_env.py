@@ -175,6 +175,7 @@ class MicroRTSGridModeVecEnv:
         bot_fusion=True,
         game_offset=0,
         _ai1s=None,
+        _extra_maps=(),
     ):
         # vec_env.py:110-127
         self.num_selfplay_envs = num_selfplay_envs
@@ -208,7 +209,7 @@ class MicroRTSGridModeVecEnv:
         # map table: one entry per distinct path; envs of a selfplay pair share game 2k's map
         full = [os.path.join(self.microrts_path, p) for p in self.map_paths]
         self._map_table = []
-        for p in full + self.cycle_maps:
+        for p in full + self.cycle_maps + [os.path.join(self.microrts_path, m) for m in _extra_maps]:
             if p not in self._map_table:
                 self._map_table.append(p)
         self._map_index = {p: i for i, p in enumerate(self._map_table)}
@@ -455,6 +456,27 @@ class MicroRTSGridModeVecEnv:
         _native.check(_native.lib().mrts_reset_games(self._h, self._stream(), ga, ma, len(games), self._obs.data_ptr()), self._h,
                       "reset_games")
 
+    def park_games(self, games):
+        """Park the given games (mrts_park_games): they stop ticking and their envs'
+        obs, masks, rewards and dones read zero until reset_games() restarts them on
+        a map.  MicroRTSSizeCyclingVecEnv parks an env's game in every size engine
+        but the one it plays in."""
+        import ctypes
+
+        games = [int(g) for g in games]
+        if not games:
+            return
+        ga = (ctypes.c_int32 * len(games))(*games)
+        _native.check(_native.lib().mrts_park_games(self._h, self._stream(), ga, len(games), self._obs.data_ptr()), self._h,
+                      "park_games")
+        envs = [e for g in games for e in self.envs_of_game(g)]
+        for t in (self._raw, self._done, self._rew, self._done0):
+            t[envs] = 0
+
+    def envs_of_game(self, g):
+        nsp2 = self.num_selfplay_envs // 2
+        return [2 * g, 2 * g + 1] if g < nsp2 else [self.num_selfplay_envs + g - nsp2]
+
     def game_stats(self):
         """(num_games, 6) int32: game time, episode env steps, steps since creation, serial
         ticks, ordered-path rows, auto-resets (mrts_game_stats)."""
@@ -696,6 +718,126 @@ class MicroRTSMixedMapVecEnv:
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
+
+    def error_flags(self):
+        f = 0
+        for e in self.envs:
+            f |= e.error_flags()
+        return f
+
+    def close(self):
+        for e in self.envs:
+            e.close()
+
+
+class MicroRTSSizeCyclingVecEnv:
+    """Map cycling across map sizes: vec_env.py:1038-1056 (a finished game restarts
+    on next(cycle_maps)) with cycle_maps of several sizes.
+
+    One engine (MicroRTSGridModeVecEnv) per map size in map_paths + cycle_maps,
+    each holding EVERY env of the batch at the same index (selfplay pairs first,
+    then bot envs -- the engine order).  An env plays in exactly one
+    engine and is parked (mrts_park_games: no tick, zero obs / masks / rewards /
+    dones) in the others.  When its game ends, the env restarts on the next cycle
+    map; if that map has another size, its game is parked in the old engine and
+    reset onto the map in the new one (an env of a selfplay pair moves with its
+    partner).  The terminal reward and done of the tick are reported first.
+
+      env = MicroRTSSizeCyclingVecEnv(4, 2, ai2s=[...], map_paths=[...], cycle_maps=[8x8, 16x16, ...])
+      obs  = env.reset()                     # list over env.sizes: (N, H_i, W_i, P) device tensors
+      mask = env.get_action_mask()           # list over env.sizes: (N, H_i*W_i, 78)
+      obs, rew, done, infos = env.step(acts) # acts: list over env.sizes; rew / done: (N,) over all envs
+      env.bucket                             # (N,) index into env.sizes of each env's current map
+
+    Rows of envs that play in another engine are zero in every list entry, so a
+    policy can run each size's batch as it is.  Device tensors only (the
+    return_tensors=True contract)."""
+
+    def __init__(self, num_selfplay_envs, num_bot_envs, ai2s=[], map_paths=["maps/16x16/basesWorkers16x16.xml"], cycle_maps=[],
+                 max_steps=2000, partial_obs=False, reward_weight=np.array([0.0, 1.0, 0.0, 0.0, 0.0, 5.0]), device=None,
+                 obs_dtype=None):
+        self.num_selfplay_envs, self.num_bot_envs = num_selfplay_envs, num_bot_envs
+        self.num_envs = num_selfplay_envs + num_bot_envs
+        root = os.path.join(gym_microrts.__path__[0], "microrts")
+        per_env = list(map_paths) * self.num_envs if len(map_paths) == 1 else list(map_paths)
+        assert len(per_env) == self.num_envs, "if multiple maps are provided, they should be provided for each environment"
+
+        def size(m):
+            r = ET.parse(os.path.join(root, m)).getroot()
+            return int(r.get("height")), int(r.get("width"))
+
+        self.sizes = sorted({size(m) for m in per_env + list(cycle_maps)})
+        self._size_of = {m: size(m) for m in per_env + list(cycle_maps)}
+        self.cycle_maps = list(cycle_maps)
+        self.next_map = cycle(self.cycle_maps)
+        self.bucket = np.array([self.sizes.index(self._size_of[m]) for m in per_env], np.int64)
+        self.envs = []
+        for i, sz in enumerate(self.sizes):
+            own = [m for m in per_env + self.cycle_maps if self._size_of[m] == sz]
+            maps_i = [m if self._size_of[m] == sz else own[0] for m in per_env]   # placeholders are parked at reset
+            self.envs.append(MicroRTSGridModeVecEnv(num_selfplay_envs, num_bot_envs, partial_obs=partial_obs, max_steps=max_steps,
+                                                    ai2s=ai2s, map_paths=maps_i, reward_weight=reward_weight, device=device,
+                                                    return_tensors=True, obs_dtype=obs_dtype, _extra_maps=own))
+        self.device = self.envs[0].device
+        self.reward_weight = reward_weight
+
+    def _games_in(self, i, inside):
+        e0 = self.envs[0]
+        return [g for g in range(e0._n_games()) if (self.bucket[e0.envs_of_game(g)[0]] == i) == inside]
+
+    def reset(self):
+        out = []
+        for i, e in enumerate(self.envs):
+            e.reset()
+            e.park_games(self._games_in(i, False))
+            out.append(e._obs)
+        return out
+
+    def get_action_mask(self):
+        return [e.get_action_mask() for e in self.envs]
+
+    def step_async(self, actions):
+        assert len(actions) == len(self.envs)
+        for e, a in zip(self.envs, actions):
+            e.step_async(a)
+
+    def step_wait(self):
+        outs = [e.step_wait() for e in self.envs]
+        # each env's row is non-zero in the engine it played the tick in only
+        rew = outs[0][1].clone()
+        done = outs[0][2].clone()
+        raw = outs[0][3]._raw.clone()
+        for _, r, d, inf in outs[1:]:
+            rew += r
+            done |= d
+            raw += inf._raw
+        self._cycle(done.cpu().numpy())
+        return [e._obs for e in self.envs], rew, done, LazyInfos(raw)
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def _cycle(self, done0):
+        if not self.cycle_maps:
+            return
+        e0 = self.envs[0]
+        moves = {}   # (from, to) -> (games, maps)
+        for e in np.nonzero(done0)[0]:
+            if e < self.num_selfplay_envs and e % 2:
+                continue
+            g = e0.game_of_env(e)
+            m = next(self.next_map)
+            src, dst = int(self.bucket[e]), self.sizes.index(self._size_of[m])
+            gl, ml = moves.setdefault((src, dst), ([], []))
+            gl.append(g)
+            ml.append(self.envs[dst]._map_index[os.path.join(self.envs[dst].microrts_path, m)])
+            for x in e0.envs_of_game(g):
+                self.bucket[x] = dst
+        for (src, dst), (gl, ml) in moves.items():
+            if src != dst:
+                self.envs[src].park_games(gl)
+            self.envs[dst].reset_games(gl, ml)
 
     def error_flags(self):
         f = 0
