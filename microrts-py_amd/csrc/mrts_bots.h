@@ -67,10 +67,17 @@ __host__ __device__ inline size_t b16(size_t x) { return (x + 15) & ~(size_t)15;
 __host__ __device__ inline size_t bot_lds_bytes(int HW, int W) {
     const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
     return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW) + b16((size_t)HW) + 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) +
-           b16(4 * 32);
+           b16(4 * 4);
 }
 
-__device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W) {
+// `tail`: where the small arrays (pend, pab, vis, sc) go when the caller keeps
+// them apart (the fused k_step's early bot, whose workgroup still reads the
+// step's scalars and visibility words while the bot runs); null = behind wall
+__host__ __device__ inline size_t bot_tail_bytes(int HW, int W) {
+    const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
+    return 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) + b16(4 * 4);
+}
+__device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W, unsigned char* tail = nullptr) {
     BL L;
     size_t o = 0;
     auto take = [&](size_t n) { unsigned char* p = base + o; o += b16(n); return p; };
@@ -83,10 +90,14 @@ __device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W) {
     L.pa = (int32_t*)take(4 * (size_t)HW);
     L.aa = (int4*)take(32 * (size_t)HW);
     L.wall = (uint8_t*)take((size_t)HW);   // at the step kernel's wall offset too (wall_shared)
+    if (tail) {
+        base = tail;
+        o = 0;
+    }
     L.pend = (uint32_t*)take(4 * posw);
     L.pab = (uint32_t*)take(4 * posw);
     L.vis = (uint32_t*)take(4 * ((size_t)HW / 32 + 1));
-    L.sc = (int*)take(4 * 32);
+    L.sc = (int*)take(4 * 4);   // pending produce cost per player, error bits
     return L;
 }
 
@@ -1136,7 +1147,7 @@ __host__ __device__ inline bool wall_shared(int HW) {
 template <bool FUSED>
 __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem,
                                          const int32_t* step_sc = nullptr, bool pre_ok = false, int4 pre_aa = int4{0, 0, 0, 0},
-                                         int4 pre_aa2 = int4{0, 0, 0, 0}) {
+                                         int4 pre_aa2 = int4{0, 0, 0, 0}, unsigned char* tail = nullptr) {
     const int g = p.nsp_games + b, lane = blane();
     const int HW = p.HW, W = p.W;
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
@@ -1148,7 +1159,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         if (lane0()) genv[w_npa] = 0;
         return;
     }
-    BL L = bot_carve(smem, HW, W);
+    BL L = bot_carve(smem, HW, W, tail);
     int4* const aa_g = p.aa + ((size_t)b * 2 + player) * HW * 2;
     int32_t* const pa_g = p.botpa + ((size_t)b * 2 + player) * HW;
     S.W = W;

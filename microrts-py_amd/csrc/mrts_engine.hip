@@ -93,7 +93,11 @@ __host__ __device__ inline size_t fb_outw_offset(int HW, int W, int NT) {
     const size_t a = lds_bytes(HW, W, NT), b = bots::bot_lds_bytes(HW, W);
     return a16(a > b ? a : b);
 }
-__host__ __device__ inline size_t fb_lds_bytes(int HW, int W, int NT) { return fb_outw_offset(HW, W, NT) + a16(32 * (size_t)HW); }
+// + the early bot's (P == 29) tail arrays and the streaming waves' phase-A counter
+__host__ __device__ inline size_t fb_tail_offset(int HW, int W, int NT) { return fb_outw_offset(HW, W, NT) + a16(32 * (size_t)HW); }
+__host__ __device__ inline size_t fb_lds_bytes(int HW, int W, int NT) {
+    return fb_tail_offset(HW, W, NT) + a16(bots::bot_tail_bytes(HW, W)) + 16;
+}
 
 __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     Lds L;
@@ -247,16 +251,20 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
 // scratch lists (resv .. snap), dead by now.
 // `skip`: lanes [0, skip) leave after phase A (the bot-fused k_step's wave 0) and
 // the others stream phase B alone.
+// `early_cnt` (the early-bot k_step): wave 0 is running the bot already, so
+// phase A too runs on lanes [skip, NT) only and its end is a counter the
+// streaming waves meet at in LDS instead of a workgroup barrier.
 template <int NT, int P, typename OT>
 __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks,
-                                             int skip = 0) {
+                                             int skip = 0, int* early_cnt = nullptr) {
     const int HW = p.HW, NV = G.nviews;
     uint32_t* ow = L.outw;            // [NV][HW]    one-hot bits
     uint32_t* mw = L.outw + 2 * HW;   // [NV][HW][3] mask bits (bit 0 = source)
     const Grid gd{p.W, p.H, HW};
     if (obs && P == 31) compute_vis<NT>(p, L);
     const int nw = HW / 32 + 1;
-    for (int c = threadIdx.x; c < HW; c += NT) {
+    const int a0 = early_cnt ? skip : 0;   // phase A's first lane
+    for (int c = (int)threadIdx.x - a0; c < HW; c += NT - a0) {
         const uint32_t u = L.unit[c], a = L.act[c];
         const uint8_t wl = L.wall[c];
         for (int v = 0; v < NV; v++) {
@@ -279,7 +287,15 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             }
         }
     }
-    __syncthreads();
+    if (early_cnt) {   // the streaming waves' own meeting point (wave 0 never arrives)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(early_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(early_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (NT - skip) / 64)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __syncthreads();
+    }
     // ---- phase B -----------------------------------------------------------
     // Bot-fused k_step (skip = 64): from here on wave 0 runs bots::bot_game, whose
     // LDS region starts at smem offset 0 and overwrites L.unit / uid / act / seq /
@@ -700,6 +716,8 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
     if (FB) L.outw = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
+    int* const early_cnt = reinterpret_cast<int*>(smem + fb_tail_offset(HW, p.W, NT) + a16(bots::bot_tail_bytes(HW, p.W)));
+    if (FB && threadIdx.x == 0) *early_cnt = 0;   // read after several barriers below
     const Grid gd{p.W, p.H, HW};
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
@@ -984,6 +1002,20 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // + getMasks of the next tick (bound mask outputs): every read of this
     //   game's source rows (phase 1) is behind the barriers above
     const bool botg = FB && g >= p.nsp_games && NT > 64;
+    if (FB && P == 29 && botg) {
+        // Early bot (full observability: the bot writes none of the arrays phase A
+        // reads -- unit / act / wall stay as stored, the step's scalars and
+        // visibility words are left alone, its small arrays go to the tail region):
+        // once store_game has read the arrays the bot reuses, wave 0 starts the
+        // next tick's bot at once while waves 1.. build the output words and
+        // stream them, meeting at an LDS counter instead of a workgroup barrier.
+        __syncthreads();
+        if (threadIdx.x < 64)
+            bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT));
+        else
+            emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, 64, early_cnt);
+        return;
+    }
     emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0);
     if (FB && botg && threadIdx.x < 64)   // every read of the stored state is behind phase A's barrier
         bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2);   // the step's arrays are dead: only L.outw is read on
