@@ -376,22 +376,29 @@ __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int r
     if (lane == sy) nbr = ((sx + 1 < S.W) ? 1u << (sx + 1) : 0u) | (sx > 0 ? 1u << (sx - 1) : 0u);
     if (lane == sy - 1 || lane == sy + 1) nbr = 1u << sx;
     const uint32_t frm = fr & rowmask;
+    auto grow_of = [&](uint32_t f, uint32_t sn) {   // the next layer: rows y-1 and y+1 of f (rows >= H hold no free cell)
+        return ((f << 1) | (f >> 1) | from_lane_below(f) | from_lane_above(f)) & frm & ~sn;
+    };
+    auto first_dir = [&](uint32_t f) {   // the layer touches a neighbour: ties UP, RIGHT, DOWN, LEFT
+        const uint32_t rU = (uint32_t)lane_value((int)f, max(sy - 1, 0)), rC = (uint32_t)lane_value((int)f, sy),
+                       rD = (uint32_t)lane_value((int)f, min(sy + 1, 63));
+        if (sy > 0 && ((rU >> sx) & 1u)) return 0;
+        if (sx + 1 < S.W && ((rC >> (sx + 1)) & 1u)) return 1;
+        if (sy + 1 < S.H && ((rD >> sx) & 1u)) return 2;
+        return 3;
+    };
+    // two layers per round, one branch for "a layer touched a neighbour" and one for
+    // "the front died": the same first touching layer and the same null path as one
+    // layer at a time (g2 is empty whenever g1 is)
     uint32_t seen = goal, front = goal;
-    for (int it = 0; it <= S.HW; it++) {
-        if (__ballot((front & nbr) != 0)) {   // first layer touching a neighbour: ties UP, RIGHT, DOWN, LEFT
-            const uint32_t rU = (uint32_t)lane_value((int)front, max(sy - 1, 0)), rC = (uint32_t)lane_value((int)front, sy),
-                           rD = (uint32_t)lane_value((int)front, min(sy + 1, 63));
-            if (sy > 0 && ((rU >> sx) & 1u)) return 0;
-            if (sx + 1 < S.W && ((rC >> (sx + 1)) & 1u)) return 1;
-            if (sy + 1 < S.H && ((rD >> sx) & 1u)) return 2;
-            return 3;
-        }
-        // rows y-1 and y+1 of the front (rows >= H hold no free cell, so nothing grows there)
-        const uint32_t up = from_lane_below(front), dn = from_lane_above(front);
-        const uint32_t grow = ((front << 1) | (front >> 1) | up | dn) & frm & ~seen;
-        seen |= grow;
-        front = grow;
-        if (!__ballot(grow != 0)) return -1;
+    for (int it = 0; it <= S.HW; it += 2) {
+        const uint32_t g1 = grow_of(front, seen), s1 = seen | g1;
+        const uint32_t g2 = grow_of(g1, s1);
+        const unsigned long long t0 = __ballot((front & nbr) != 0), t1 = __ballot((g1 & nbr) != 0);
+        if (t0 | t1) return first_dir(t0 ? front : g1);
+        if (!__ballot(g2 != 0)) return -1;
+        seen = s1 | g2;
+        front = g2;
     }
     return -1;
 }
@@ -1195,7 +1202,15 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     }
     for (int i = lane; i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
     for (int i = lane; i < visw; i += BT) L.vis[i] = 0;
-    for (int i = lane; i < 2 * S.naa; i += BT) L.aa[i] = (FUSED && pre_ok && i < 2 * BT) ? (i < BT ? pre_aa : pre_aa2) : aa_g[i];
+    {   // the abstract actions: the first 128 words come prefetched in registers when fused
+        int i0 = 0;
+        if (FUSED && pre_ok) {   // no global load is issued for them
+            if (lane < 2 * S.naa) L.aa[lane] = pre_aa;
+            if (BT + lane < 2 * S.naa) L.aa[BT + lane] = pre_aa2;
+            i0 = 2 * BT;
+        }
+        for (int i = i0 + lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
+    }
     if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     bot_sync<FUSED>();
     // cells observable by the bot's player (PartiallyObservableGameState);

@@ -302,6 +302,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     // aux / vis / sc.  Phase B must read nothing but the output words `ow` / `mw`
     // (their own region at fb_outw_offset) and kernel parameters.
     if ((int)threadIdx.x < skip) return;
+    __builtin_amdgcn_s_setprio(0);
     const int t0 = (int)threadIdx.x - skip, nt = NT - skip;
     if (obs) {
         OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P;
@@ -718,6 +719,10 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     if (FB) L.outw = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
     int* const early_cnt = reinterpret_cast<int*>(smem + fb_tail_offset(HW, p.W, NT) + a16(bots::bot_tail_bytes(HW, p.W)));
     if (FB && threadIdx.x == 0) *early_cnt = 0;   // read after several barriers below
+    // issue priority: the game logic (latency-bound chains of LDS steps and
+    // barriers) over other workgroups' output streams (memory-bound), which
+    // drop to 0 in emit_outputs' phase B
+    __builtin_amdgcn_s_setprio(2);
     const Grid gd{p.W, p.H, HW};
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
@@ -1010,8 +1015,10 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         // next tick's bot at once while waves 1.. build the output words and
         // stream them, meeting at an LDS counter instead of a workgroup barrier.
         __syncthreads();
-        if (threadIdx.x < 64)
+        if (threadIdx.x < 64) {
+            __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
             bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT));
+        }
         else
             emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, 64, early_cnt);
         return;
