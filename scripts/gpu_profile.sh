@@ -17,4 +17,7 @@ timeout -k 10 300 python bench.py > "$O/bench.json" 2> "$O/bench.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt" -o kt -- python3 $BENCH > "$O/bench_kt.json" 2> "$O/kt.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$O/fetch" -o fetch -- python3 $BENCH --no-kernel-events > "$O/bench_fetch.json" 2> "$O/fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$O/write" -o write -- python3 $BENCH --no-kernel-events > "$O/bench_write.json" 2> "$O/write.err"
+# configs[1] (1024 envs vs device coacAI): the kernel trace of its bench command too
+COAC="bench.py --workload coac --envs-per-gpu 1024 --steps 300 --warmup 20 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt_coac" -o kt -- python3 $COAC > "$O/bench_coac_kt.json" 2> "$O/kt_coac.err"
 echo done > "$O/DONE"
