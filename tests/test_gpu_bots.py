@@ -161,9 +161,11 @@ def test_league_outcomes_on_device():
     assert g.error_flags() == 0
 
 
-def test_mixed_map_buckets_match_oracle():
+@pytest.mark.parametrize("concurrent", [False, True])
+def test_mixed_map_buckets_match_oracle(concurrent):
     """BASELINE configs[4]: 8x8 / 16x16 / 24x24 buckets in one MicroRTSMixedMapVecEnv,
-    selfplay + device workerRush / coacAI envs, every bucket bit-exact vs its oracle."""
+    selfplay + device workerRush / coacAI envs, every bucket bit-exact vs its oracle
+    (buckets back to back, and each on its own HIP stream)."""
     import torch
 
     from gym_microrts import microrts_ai
@@ -175,8 +177,8 @@ def test_mixed_map_buckets_match_oracle():
             ("maps/24x24/basesWorkers24x24.xml", 4, ["workerRushAI", "coacAI"])]
     w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
     env = MicroRTSMixedMapVecEnv([dict(map_paths=[m], num_selfplay_envs=nsp, ai2s=[getattr(microrts_ai, a) for a in ais])
-                                  for m, nsp, ais in spec], max_steps=300, return_tensors=True, reward_weight=w,
-                                 obs_dtype=torch.int32)
+                                  for m, nsp, ais in spec], concurrent=concurrent, max_steps=300, return_tensors=True,
+                                 reward_weight=w, obs_dtype=torch.int32)
     orc = [OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, m)], max_steps=300, ai2s=ais, reward_weight=w)
            for m, nsp, ais in spec]
     for og, oo in zip(env.reset(), [o.reset() for o in orc]):
