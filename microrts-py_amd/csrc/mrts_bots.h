@@ -387,18 +387,21 @@ __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int r
         if (sy + 1 < S.H && ((rD >> sx) & 1u)) return 2;
         return 3;
     };
-    // two layers per round, one branch for "a layer touched a neighbour" and one for
+    // four layers per round, one branch for "a layer touched a neighbour" and one for
     // "the front died": the same first touching layer and the same null path as one
-    // layer at a time (g2 is empty whenever g1 is)
+    // layer at a time (a layer after an empty one is empty too)
     uint32_t seen = goal, front = goal;
-    for (int it = 0; it <= S.HW; it += 2) {
+    for (int it = 0; it <= S.HW; it += 4) {
         const uint32_t g1 = grow_of(front, seen), s1 = seen | g1;
-        const uint32_t g2 = grow_of(g1, s1);
+        const uint32_t g2 = grow_of(g1, s1), s2 = s1 | g2;
+        const uint32_t g3 = grow_of(g2, s2), s3 = s2 | g3;
+        const uint32_t g4 = grow_of(g3, s3);
         const unsigned long long t0 = __ballot((front & nbr) != 0), t1 = __ballot((g1 & nbr) != 0);
-        if (t0 | t1) return first_dir(t0 ? front : g1);
-        if (!__ballot(g2 != 0)) return -1;
-        seen = s1 | g2;
-        front = g2;
+        const unsigned long long t2 = __ballot((g2 & nbr) != 0), t3 = __ballot((g3 & nbr) != 0);
+        if (t0 | t1 | t2 | t3) return first_dir(t0 ? front : t1 ? g1 : t2 ? g2 : g3);
+        if (!__ballot(g4 != 0)) return -1;
+        seen = s3 | g4;
+        front = g4;
     }
     return -1;
 }
