@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--envs-per-gpu", type=int, default=8192)
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--seeds", type=int, default=1,
+                    help="independent runs with seeds seed, seed+1, ... (fresh env, pre-roll, warmup and K timed steps "
+                         "each); the line reports the median run (BASELINE.md §3: median of 3 seeds) and every seed's value")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
@@ -463,7 +466,20 @@ def main():
         torch.cuda.set_device(local_rank)
         elapsed, kern, flags, hw, G, N, P, src_rows, stats = run_mixed(args, rank, torch.device("cuda", local_rank))
     else:
-        elapsed, kern, flags, hw, G, N, P, src_rows, stats = run_gpu(args, rank, world, local_rank)
+        runs = []
+        for i in range(max(1, args.seeds)):
+            a = argparse.Namespace(**vars(args))
+            a.seed = args.seed + i
+            runs.append((a.seed, run_gpu(a, rank, world, local_rank)))
+        order = sorted(range(len(runs)), key=lambda i: runs[i][1][0])
+        elapsed, kern, flags, hw, G, N, P, src_rows, stats = runs[order[len(order) // 2]][1]
+        if len(runs) > 1:
+            stats["seeds"] = {"median_of": len(runs), "seed_of_median": runs[order[len(order) // 2]][0],
+                              "values": {str(sd): round(N * args.steps / r[0], 1) for sd, r in runs},
+                              "note": "per-rank values; the reported line is the median-elapsed run"}
+            flags = 0
+            for _, r in runs:
+                flags |= r[2]
     dev = torch.device("cuda", local_rank)
     elapsed_max = max_over_ranks(elapsed, world, dev)
     total_env_steps = world * N * args.steps
