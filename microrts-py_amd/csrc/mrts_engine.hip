@@ -124,9 +124,13 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     return L;
 }
 
-// Ordered block-wide compaction: list <- cells c (ascending) with pred(c).
-template <int NT, typename F>
-__device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsigned long long* s_mask) {
+// Ordered block-wide compaction: list <- cells c (ascending) with pred(c);
+// put(position, c) is called for every entry as it is written.
+struct NoPut {
+    __device__ void operator()(int, int) const {}
+};
+template <int NT, typename F, typename G = NoPut>
+__device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsigned long long* s_mask, G put = G()) {
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int J = (HW + NT - 1) / NT;
@@ -147,7 +151,11 @@ __device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsi
             if (j == 0) total += pc;
         }
         unsigned long long m = s_mask[mi];
-        if ((m >> lane) & 1ull) list[before + __popcll(m & ((1ull << lane) - 1ull))] = j * NT + threadIdx.x;
+        if ((m >> lane) & 1ull) {
+            const int pos = before + __popcll(m & ((1ull << lane) - 1ull)), c = j * NT + threadIdx.x;
+            list[pos] = c;
+            put(pos, c);
+        }
     }
     __syncthreads();
     return total;
@@ -903,19 +911,24 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         uint32_t a = L.act[c];
         if (a && act_done(a) <= now && code_type(act_code(a)) == A_NONE) L.act[c] = 0;
     }
+    // (the ready cells' sequence words go to L.aux, dead since the issue, in list order)
     int nready = compact_cells<NT>(HW, [&](int c) {
         uint32_t a = L.act[c];
         return a != 0 && act_done(a) <= now;
-    }, L.list, L.ballot);
+    }, L.list, L.ballot, [&](int pos, int c) { L.aux[pos] = L.seq[c]; });
     // snapshots of the ready assignments in LinkedHashMap (issue-sequence)
     // order: lane-parallel rank by sequence word (unique among non-NONE actions)
     const int posw = (HW + 2 * p.W) / 32 + 1;
     for (int i = threadIdx.x; i < posw; i += NT) L.claim[i] = 0;
     for (int i = threadIdx.x; i < nready; i += NT) {
         const int c = L.list[i];
-        const uint32_t sq = L.seq[c];
-        int rank = 0;
-        for (int j = 0; j < nready; j++) rank += L.seq[L.list[j]] < sq;
+        const uint32_t sq = L.aux[i];
+        int rank = 0, j = 0;
+        for (; j + 4 <= nready; j += 4) {   // four sequence words per LDS read, no pointer chase
+            const uint4 v = *reinterpret_cast<const uint4*>(L.aux + j);
+            rank += (v.x < sq) + (v.y < sq) + (v.z < sq) + (v.w < sq);
+        }
+        for (; j < nready; j++) rank += L.aux[j] < sq;
         L.snap[rank] = make_int4(c, (int)L.unit[c], act_code(L.act[c]), L.uid[c]);
     }
     __syncthreads();
