@@ -57,7 +57,7 @@ struct Lds {
 // L.sc[0 .. MRTS_GENV_WORDS) mirrors genv (load_game / store_game)
 enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_UID = MRTS_G_NEXT_UID,
        SC_STEPS = MRTS_G_STEPS, SC_MAP = MRTS_G_MAP, SC_ERR = MRTS_G_ERR, SC_AA_N = MRTS_G_AA_N, SC_TICKS = MRTS_G_TICKS,
-       SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_WORDS = 32 };
+       SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_RPROD = 29 /* ready produces */, SC_WORDS = 32 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -920,6 +920,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // order: lane-parallel rank by sequence word (unique among non-NONE actions)
     const int posw = (HW + 2 * p.W) / 32 + 1;
     for (int i = threadIdx.x; i < posw; i += NT) L.claim[i] = 0;
+    if (threadIdx.x == 0) L.sc[SC_RPROD] = 0;
     for (int i = threadIdx.x; i < nready; i += NT) {
         const int c = L.list[i];
         const uint32_t sq = L.aux[i];
@@ -935,17 +936,19 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // Independent ready sets (no attack, no two harvests of one pile) commute:
     // every target cell is distinct (moves / produces hold reservations),
     // resources only add up, and produced units take ids in issue order.
-    int serial = 0;
+    int serial = 0, nprodr = 0;
     for (int i = threadIdx.x; i < nready; i += NT) {
         L.act[L.list[i]] = 0;   // unitActions.remove
         const int4 sn = L.snap[i];
         const int ty = code_type(sn.z);
         if (ty == A_ATTACK) serial = 1;
+        nprodr += ty == A_PRODUCE;
         if (ty == A_HARVEST) {
             const int n = nb_cell(gd, sn.x, code_param(sn.z));
             if (n >= 0 && (atomicOr(&L.claim[n >> 5], 1u << (n & 31)) >> (n & 31)) & 1u) serial = 1;
         }
     }
+    if (nprodr) atomicAdd(&L.sc[SC_RPROD], nprodr);   // the ids the produced units take
     serial = __syncthreads_or(serial);
     if (serial) {
         if (threadIdx.x == 0)
@@ -969,7 +972,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         L.sc[MRTS_G_ORDERED] += nrows;
         if (now >= MRTS_MAX_TIME) L.sc[SC_ERR] |= MRTS_ERR_TIME_OVERFLOW;
         if (!serial)
-            for (int i = 0; i < nready; i++) L.sc[SC_UID] += code_type(L.snap[i].z) == A_PRODUCE;
+            L.sc[SC_UID] += L.sc[SC_RPROD];
     }
     __syncthreads();
     // (5) PhysicalGameState.gameover / winner
