@@ -266,18 +266,39 @@ def kernel_bytes(G, N, HW, P=29, eager=True, sampler="src", src_rows=0):
 PMC_NAMES = {"get_masks": "k_masks", "step": "k_step", "sample": "k_sample"}
 
 
-def pmc_traffic(kernel):
+LIB = os.path.join(REPO, "microrts-py_amd", "gym_microrts", "libmicrorts_amd.so")
+
+
+def lib_sha256():
+    import hashlib
+
+    h = hashlib.sha256()
+    with open(LIB, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_latest.json, written by scripts/pmc_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command)."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command, filed
+    under `workload` = <workload>@<envs per gpu>).  Only counters of THIS build
+    count: the summary's library sha256 must equal the running library's, else
+    (None, reason)."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
-        return None, None
+        return None, "no profiles/pmc_latest.json"
     d = json.load(open(path))
-    for k, v in d.items():
+    if d.get("_meta", {}).get("lib_sha256") != lib_sha256():
+        return None, "profiles/pmc_latest.json is of another build (lib sha256 differs): traffic not reported"
+    w = d.get("workloads", {}).get(workload)
+    if not w:
+        return None, f"no PMC passes for {workload} in profiles/pmc_latest.json"
+    for k, v in w["kernels"].items():
         if k.startswith(PMC_NAMES.get(kernel, "?")) and v.get("hbm_bytes"):
-            return v["hbm_bytes"], "profiles/pmc_latest.json"
-    return None, None
+            return v["hbm_bytes"], f"profiles/pmc_latest.json [{workload}] {k}, lib sha256 {d['_meta']['lib_sha256'][:12]}"
+    return None, f"no {kernel} counters for {workload}"
 
 
 def run_gpu(args, rank, world, local_rank):
@@ -499,9 +520,10 @@ def main():
         dom = max((k for k in kern if k in kb), key=lambda k: kern[k], default=None)
         if dom:
             achieved = kb[dom] / (kern[dom] * 1e-3) / 1e9
-            # the committed PMC summary is of the headline command (selfplay, 8192 envs) only
-            headline = args.workload == "selfplay" and N == 8192 and args.api == "tensor"
-            traffic, tsrc = pmc_traffic(dom) if headline else (None, None)
+            # the committed PMC summary covers the default bench commands of a workload
+            # (tensor api, eager masks, source-guided sampler) at one env count
+            default_cmd = args.api == "tensor" and eager and args.sampler == "src"
+            traffic, tsrc = pmc_traffic(dom, f"{args.workload}@{N}") if default_cmd else (None, "non-default bench options")
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else round(traffic / (kern[dom] * 1e-3) / 1e9, 1),

@@ -13,9 +13,20 @@ envs) runs end to end on the GPU.
 
   --api numpy  : the reference's return contract (numpy obs / masks / rewards),
                  i.e. the host round trips ppo_gridnet.py performs every step
+  --api hybrid : the contract an UNMODIFIED ppo_gridnet.py gets with
+                 MICRORTS_AMD_RETURN=hybrid (or `run_driver --contract hybrid`):
+                 obs / masks stay device tensors, rewards / dones / infos numpy
   --api tensor : return_tensors=True, every buffer stays in HBM
 
-  python examples/ppo_gridnet_driver.py --num-selfplay-envs 4096 --partial-obs --num-steps 8 --updates 2 --api tensor
+With --api numpy / hybrid the rollout makes ppo_gridnet.py's own calls in its own
+forms (`torch.Tensor(envs.reset()).to(device)`, `torch.tensor(envs.get_action_mask())
+.to(device)`, `envs.step(action.cpu().numpy().reshape(n, -1))`, `torch.Tensor(rs)`,
+the `info["episode"]` scan; ppo_gridnet.py:421, 466, 475-490) through its wrapper
+stack: MicroRTSStatsRecorder (restated below, ppo_gridnet.py:126-160) inside
+VecMonitor (ppo_gridnet.py:384-385).  The contract is chosen by the environment
+variable alone: the env is constructed without `return_tensors`.
+
+  python examples/ppo_gridnet_driver.py --num-selfplay-envs 4072 --num-bot-envs 24 --partial-obs --num-steps 8 --updates 2 --api hybrid
 """
 import argparse
 import json
@@ -31,6 +42,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 
 from gym_microrts import microrts_ai  # noqa: E402
 from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv  # noqa: E402
+from gym_microrts.run_driver import install as _install_compat  # noqa: E402
+
+_install_compat()   # stable_baselines3 stand-ins when the real package is absent (as on the GPU host)
+from stable_baselines3.common.vec_env import VecEnvWrapper, VecMonitor  # noqa: E402
 
 NVEC = [6, 4, 4, 4, 4, 7, 49]   # action_plane_space.nvec (vec_env.py:234)
 
@@ -61,6 +76,58 @@ class GridNet(nn.Module):
         return logits, self.v(z).squeeze(-1)
 
 
+class StatsRecorder(VecEnvWrapper):
+    """MicroRTSStatsRecorder (ppo_gridnet.py:126-160), restated: per env it keeps the
+    raw reward rows of the running episode and the same rows scaled by gamma**t with
+    their sum appended; when the env's episode ends, a copy of its info gets
+    "microrts_stats" = the summed rows under the reward functions' names (and
+    "discounted_<name>", "discounted"), and the env's record starts afresh.  Reads
+    dones[i] and infos[i]["raw_rewards"] per env, as the reference does."""
+
+    def __init__(self, env, gamma=0.99):
+        super().__init__(env)
+        self.gamma = gamma
+
+    def reset(self):
+        obs = self.venv.reset()
+        self._rows = [[] for _ in range(self.num_envs)]
+        self._disc = [[] for _ in range(self.num_envs)]
+        self._t = np.zeros(self.num_envs, dtype=np.float32)
+        return obs
+
+    def step_wait(self):
+        obs, rews, dones, infos = self.venv.step_wait()
+        out = list(infos[:])
+        names = [str(rf) for rf in self.rfs]
+        dnames = ["discounted_" + k for k in names] + ["discounted"]
+        for i in range(len(dones)):
+            r = infos[i]["raw_rewards"]
+            self._rows[i].append(r)
+            self._disc[i].append((self.gamma ** self._t[i]) * np.concatenate((r, r.sum()), axis=None))
+            self._t[i] += 1
+            if dones[i]:
+                info = infos[i].copy()
+                stats = dict(zip(names, np.array(self._rows[i]).sum(0)))
+                stats.update(zip(dnames, np.array(self._disc[i]).sum(0)))
+                info["microrts_stats"] = stats
+                self._rows[i], self._disc[i], self._t[i] = [], [], 0
+                out[i] = info
+        return obs, rews, dones, out
+
+
+def make_envs(num_selfplay_envs, num_bot_envs, partial_obs, dev, max_steps=2000, **kw):
+    """ppo_gridnet.py:364-385's env: its constructor arguments (one training map,
+    cycling over it, reward_weight [10, 1, 1, 0.2, 1, 4], its bot mix), no
+    `return_tensors` (the contract comes from MICRORTS_AMD_RETURN), wrapped in
+    StatsRecorder and VecMonitor."""
+    env = MicroRTSGridModeVecEnv(num_selfplay_envs=num_selfplay_envs, num_bot_envs=num_bot_envs, partial_obs=partial_obs,
+                                 max_steps=max_steps, render_theme=2, ai2s=bot_list(num_bot_envs) if num_bot_envs else [],
+                                 map_paths=["maps/16x16/basesWorkers16x16A.xml"],
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]),
+                                 cycle_maps=["maps/16x16/basesWorkers16x16A.xml"], device=dev, **kw)
+    return VecMonitor(StatsRecorder(env, 0.99)), env
+
+
 def masked_log_softmax(logits, mask):
     """Per action component: the logit where the mask allows it, -1e8 elsewhere
     (ppo_gridnet's CategoricalMasked rule), as log-probabilities."""
@@ -88,15 +155,29 @@ def bot_list(n):
 
 
 def run(num_selfplay_envs=2, num_bot_envs=0, partial_obs=False, num_steps=16, updates=2, api="numpy", minibatches=4,
-        epochs=2, seed=1, device="cuda", log=print):
+        epochs=2, seed=1, device="cuda", log=print, max_steps=2000):
     torch.manual_seed(seed)
     np.random.seed(seed)
     dev = torch.device(device)
-    envs = MicroRTSGridModeVecEnv(num_selfplay_envs=num_selfplay_envs, num_bot_envs=num_bot_envs, partial_obs=partial_obs,
-                                  max_steps=2000, render_theme=2, ai2s=bot_list(num_bot_envs) if num_bot_envs else [],
-                                  map_paths=["maps/16x16/basesWorkers16x16A.xml"],
-                                  reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]),
-                                  cycle_maps=["maps/16x16/basesWorkers16x16A.xml"], device=dev, return_tensors=api == "tensor")
+    ref_calls = api in ("numpy", "hybrid")   # ppo_gridnet.py's own call forms + wrapper stack
+    if ref_calls:
+        prev = os.environ.get("MICRORTS_AMD_RETURN")
+        os.environ["MICRORTS_AMD_RETURN"] = api
+        try:
+            envs, base = make_envs(num_selfplay_envs, num_bot_envs, partial_obs, dev, max_steps=max_steps)
+        finally:
+            if prev is None:
+                os.environ.pop("MICRORTS_AMD_RETURN", None)
+            else:
+                os.environ["MICRORTS_AMD_RETURN"] = prev
+        assert base.contract == api
+    else:
+        base = envs = MicroRTSGridModeVecEnv(num_selfplay_envs=num_selfplay_envs, num_bot_envs=num_bot_envs,
+                                             partial_obs=partial_obs, max_steps=max_steps, render_theme=2,
+                                             ai2s=bot_list(num_bot_envs) if num_bot_envs else [],
+                                             map_paths=["maps/16x16/basesWorkers16x16A.xml"],
+                                             reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]),
+                                             cycle_maps=["maps/16x16/basesWorkers16x16A.xml"], device=dev, return_tensors=True)
     n, hw = envs.num_envs, envs.height * envs.width
     h, w, planes = envs.observation_space.shape
     net = GridNet(planes, h, w).to(dev)
@@ -109,30 +190,38 @@ def run(num_selfplay_envs=2, num_bot_envs=0, partial_obs=False, num_steps=16, up
     def as_dev(x):
         return (x if torch.is_tensor(x) else torch.from_numpy(np.asarray(x))).to(dev).float()
 
-    next_obs = as_dev(envs.reset())
+    next_obs = torch.Tensor(envs.reset()).to(dev) if ref_calls else as_dev(envs.reset())   # ppo_gridnet.py:421
     next_done = torch.zeros(n, device=dev)
     ep_ret, finished = torch.zeros(n, device=dev), []
-    steps, t0, stats = 0, time.time(), {}
+    steps, t0, stats, stats_seen = 0, time.time(), {}, 0
     rollout_s = 0.0
     for update in range(updates):
         tr = time.time()
         for t in range(num_steps):
             buf_obs[t], buf_done[t] = next_obs, next_done
             with torch.no_grad():
-                buf_mask[t] = as_dev(envs.get_action_mask())
+                if ref_calls:   # ppo_gridnet.py:466
+                    buf_mask[t] = torch.tensor(envs.get_action_mask()).to(dev)
+                else:
+                    buf_mask[t] = as_dev(envs.get_action_mask())
                 a, logp, _, v = policy(net, next_obs, buf_mask[t], hw)
             buf_act[t], buf_logp[t], buf_val[t] = a, logp, v
-            if api == "numpy":   # ppo_gridnet.py:475: host int64 actions, (N, H*W*7)
-                obs, rew, done, infos = envs.step(a.cpu().numpy().reshape(n, -1))
-                raw = torch.from_numpy(np.array([i["raw_rewards"] for i in infos])).to(dev)
+            if ref_calls:   # ppo_gridnet.py:475-490: host int64 actions (N, H*W*7), numpy rewards / dones, info scan
+                obs, rs, ds, infos = envs.step(a.cpu().numpy().reshape(n, -1))
+                next_obs = torch.Tensor(obs).to(dev)
+                buf_rew[t], next_done = torch.Tensor(rs).to(dev), torch.Tensor(ds).to(dev)
+                for info in infos:
+                    if "episode" in info.keys():
+                        finished.append(info["episode"]["r"])
+                        stats_seen += "microrts_stats" in info
             else:
                 obs, rew, done, infos = envs.step(a)
                 raw = infos._raw
-            next_obs, buf_rew[t], next_done = as_dev(obs), as_dev(rew), as_dev(done)
-            ep_ret += (raw @ torch.as_tensor(envs.reward_weight, device=dev)).float()
-            if bool(next_done.any()):
-                finished += ep_ret[next_done.bool()].tolist()
-                ep_ret[next_done.bool()] = 0
+                next_obs, buf_rew[t], next_done = as_dev(obs), as_dev(rew), as_dev(done)
+                ep_ret += (raw @ torch.as_tensor(envs.reward_weight, device=dev)).float()
+                if bool(next_done.any()):
+                    finished += ep_ret[next_done.bool()].tolist()
+                    ep_ret[next_done.bool()] = 0
             steps += n
         torch.cuda.synchronize(dev)
         rollout_s += time.time() - tr
@@ -168,9 +257,10 @@ def run(num_selfplay_envs=2, num_bot_envs=0, partial_obs=False, num_steps=16, up
         torch.cuda.synchronize(dev)
         stats = {"update": update + 1, "global_step": steps, "sps": round(steps / (time.time() - t0), 1),
                  "rollout_env_steps_per_s": round(steps / rollout_s, 1), "loss": float(loss.detach()), "policy_loss": float(pg.detach()),
-                 "value_loss": float(vl.detach()), "entropy": float(ent.detach().mean()), "episodes": len(finished)}
+                 "value_loss": float(vl.detach()), "entropy": float(ent.detach().mean()), "episodes": len(finished),
+                 "microrts_stats_infos": stats_seen, "api": api, "num_envs": n, "partial_obs": bool(partial_obs)}
         log(stats)
-    stats["engine_error_flags"] = envs.error_flags()
+    stats["engine_error_flags"] = base.error_flags()
     stats["finite"] = bool(np.isfinite([stats["loss"], stats["value_loss"], stats["entropy"]]).all())
     envs.close()
     return stats
@@ -184,8 +274,9 @@ if __name__ == "__main__":
     ap.add_argument("--num-steps", type=int, default=16)
     ap.add_argument("--updates", type=int, default=2)
     ap.add_argument("--minibatches", type=int, default=4)
-    ap.add_argument("--api", choices=["numpy", "tensor"], default="numpy")
+    ap.add_argument("--api", choices=["numpy", "hybrid", "tensor"], default="numpy")
+    ap.add_argument("--max-steps", type=int, default=2000)
     a = ap.parse_args()
     out = run(a.num_selfplay_envs, a.num_bot_envs, a.partial_obs, a.num_steps, a.updates, a.api, a.minibatches,
-              log=lambda s: print(json.dumps(s), flush=True))
+              log=lambda s: print(json.dumps(s), flush=True), max_steps=a.max_steps)
     print(json.dumps(out))

@@ -204,6 +204,13 @@ int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t si
 /* Engine invariant violations recorded on the device (OR over games). */
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out);
 
+/* Diagnostics of the bot-fused step kernel for a map size (no device work, no
+ * handle): 1 = the bot may start beside the output words' build (its LDS writes
+ * and that phase's reads / writes are disjoint, checked from both carves),
+ * 0 = fusable but the bot waits for that phase, -1 = no bot fusion for this
+ * size.  No reference counterpart (an engine-internal schedule). */
+int mrts_fused_layout_ok(int32_t width, int32_t height);
+
 /* UnitTypeTable JSON as rts.units.UnitTypeTable.toJSON / sendUTT()
  * (vec_env.py:276).  Valid for the lifetime of the handle. */
 const char *mrts_utt_json(const mrts_vec *h);

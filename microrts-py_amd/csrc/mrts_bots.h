@@ -77,7 +77,7 @@ __host__ __device__ inline size_t bot_tail_bytes(int HW, int W) {
     const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
     return 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) + b16(4 * 4);
 }
-__device__ __forceinline__ BL bot_carve(unsigned char* base, int HW, int W, unsigned char* tail = nullptr) {
+__host__ __device__ inline BL bot_carve(unsigned char* base, int HW, int W, unsigned char* tail = nullptr) {
     BL L;
     size_t o = 0;
     auto take = [&](size_t n) { unsigned char* p = base + o; o += b16(n); return p; };
@@ -1157,7 +1157,8 @@ __host__ __device__ inline bool wall_shared(int HW) {
 template <bool FUSED>
 __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem,
                                          const int32_t* step_sc = nullptr, bool pre_ok = false, int4 pre_aa = int4{0, 0, 0, 0},
-                                         int4 pre_aa2 = int4{0, 0, 0, 0}, unsigned char* tail = nullptr) {
+                                         int4 pre_aa2 = int4{0, 0, 0, 0}, unsigned char* tail = nullptr,
+                                         const uint8_t* step_wall = nullptr) {
     const int g = p.nsp_games + b, lane = blane();
     const int HW = p.HW, W = p.W;
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
@@ -1170,6 +1171,9 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         return;
     }
     BL L = bot_carve(smem, HW, W, tail);
+    // the early fused bot reads the step's terrain in place: the waves beside it
+    // read it too, and its own wall slot may overlap it (mrts_engine.hip early_bot_disjoint)
+    if (step_wall) L.wall = const_cast<uint8_t*>(step_wall);
     int4* const aa_g = p.aa + ((size_t)b * 2 + player) * HW * 2;
     int32_t* const pa_g = p.botpa + ((size_t)b * 2 + player) * HW;
     S.W = W;
@@ -1201,7 +1205,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
             L.uid[c] = v.y;
             L.act[c] = (uint32_t)v.z;
         }
-        if (!FUSED || !wall_shared(HW)) L.wall[c] = p.map_wall[(size_t)map * HW + c];
+        if (!FUSED || (!step_wall && !wall_shared(HW))) L.wall[c] = p.map_wall[(size_t)map * HW + c];
     }
     for (int i = lane; i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
     for (int i = lane; i < visw; i += BT) L.vis[i] = 0;

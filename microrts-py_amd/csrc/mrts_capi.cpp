@@ -338,6 +338,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     p.botpa = h->nbot_active ? (int32_t *)(h->ws + h->off_botpa) : nullptr;
     p.nbot_active = h->nbot_active;
     p.game_offset = h->game_offset;
+    p.early_bot = mrts_engine_early_bot_ok(h->HW, h->W);
     p.parked = nullptr;   // until a game is parked
     h->parked.assign(h->ngames, 0);
     h->err.clear();
@@ -619,6 +620,13 @@ int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {
     for (int g = 0; g < h->ngames; g++) f |= genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_ERR];
     *flags_out = f;
     return MRTS_OK;
+}
+
+int mrts_fused_layout_ok(int32_t width, int32_t height) {
+    if (width <= 0 || height <= 0 || width > 32 || height > 64) return -1;
+    const int HW = width * height;
+    if (HW <= 64 || mrts_engine_fused_lds_bytes(HW, width) > 163840) return -1;
+    return mrts_engine_early_bot_ok(HW, width);
 }
 
 const char *mrts_utt_json(const mrts_vec *h) { return h ? h->utt.c_str() : ""; }

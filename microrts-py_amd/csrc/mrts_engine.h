@@ -37,6 +37,7 @@ struct EngineParams {
     int bot_ngames;
     int fuse_bots;          // k_step: wave 0 of each bot game's workgroup decides the next tick's bot actions
     int game_offset;        // global index of game 0 (a shard of a larger batch): keys the bots' RNG
+    int early_bot;          // fused k_step: the bot may start beside phase A (mrts_engine_early_bot_ok for this size)
     const uint8_t *parked;  // [G] 1 = parked (mrts_park_games): no tick, no masks / bots, zero outputs at
                             // reset; null while no game was ever parked
 };
@@ -55,5 +56,6 @@ hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, in
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);
 size_t mrts_engine_fused_lds_bytes(int HW, int W);
+int mrts_engine_early_bot_ok(int HW, int W);
 }
 #endif

@@ -99,7 +99,7 @@ __host__ __device__ inline size_t fb_lds_bytes(int HW, int W, int NT) {
     return fb_tail_offset(HW, W, NT) + a16(bots::bot_tail_bytes(HW, W)) + 16;
 }
 
-__device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
+__host__ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     Lds L;
     size_t o = 0;
     auto take = [&](size_t n) { unsigned char* p = base + o; o += a16(n); return p; };
@@ -122,6 +122,44 @@ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
     L.vis = (uint32_t*)take(8 * (size_t)(HW / 32 + 1));
     L.claim = (uint32_t*)take(8 * (size_t)((HW + 2 * W) / 32 + 1));
     return L;
+}
+
+// The early-bot k_step (FB, P == 29): while wave 0 runs bots::bot_game (its
+// small arrays in the tail region, the step's terrain read in place), waves 1..
+// run emit_outputs' phase A, which reads the step's unit / act / wall / scalars
+// and writes the output words and the meeting counter.  True when, for this map
+// size, the bot writes none of those bytes and phase A writes none the bot reads
+// -- computed from the two carves themselves -- and the bot's unit / uid / act
+// arrays are the step's (it reads the state just stored in place).  The host
+// takes the early path only then (EngineParams::early_bot; mrts_fused_layout_ok).
+__host__ __device__ inline size_t fb_early_cnt_offset(int HW, int W, int NT) {
+    return fb_tail_offset(HW, W, NT) + a16(bots::bot_tail_bytes(HW, W));
+}
+__host__ __device__ inline bool early_bot_disjoint(int HW, int W, int NT) {
+    unsigned char* const z = reinterpret_cast<unsigned char*>((size_t)1 << 20);   // any base: only offsets matter
+    const Lds S = carve(z, HW, W, NT);
+    const bots::BL B = bots::bot_carve(z, HW, W, z + fb_tail_offset(HW, W, NT));
+    struct R {
+        const void* p;
+        size_t n;
+    };
+    auto lo = [&](const R& r) { return (size_t)((const unsigned char*)r.p - z); };
+    auto overlap = [&](const R& a, const R& b) { return lo(a) < lo(b) + b.n && lo(b) < lo(a) + a.n; };
+    const size_t hw = (size_t)HW, posw = (size_t)(HW + 2 * W) / 32 + 1, visw = (size_t)HW / 32 + 1;
+    if (B.unit != S.unit || B.uid != S.uid || B.act != S.act) return false;
+    const R bot_w[8] = {{B.ucell, 4 * hw}, {B.uuid, 4 * hw}, {B.pa, 4 * hw}, {B.aa, 32 * hw},
+                        {B.pend, 4 * posw}, {B.pab, 4 * posw}, {B.vis, 4 * visw}, {B.sc, 16}};
+    const R bot_r[4] = {{B.unit, 4 * hw}, {B.uid, 4 * hw}, {B.act, 4 * hw}, {S.wall, hw}};
+    const R a_r[4] = {{S.unit, 4 * hw}, {S.act, 4 * hw}, {S.wall, hw}, {S.sc, 4 * (size_t)SC_WORDS}};
+    const R a_w[2] = {{z + fb_outw_offset(HW, W, NT), 32 * hw}, {z + fb_early_cnt_offset(HW, W, NT), 4}};
+    for (const R& b : bot_w) {
+        if (lo(b) + b.n > fb_lds_bytes(HW, W, NT)) return false;
+        for (const R& a : a_r) if (overlap(a, b)) return false;
+        for (const R& a : a_w) if (overlap(a, b)) return false;
+    }
+    for (const R& a : a_w)
+        for (const R& b : bot_r) if (overlap(a, b)) return false;
+    return true;
 }
 
 // Ordered block-wide compaction: list <- cells c (ascending) with pred(c);
@@ -357,17 +395,22 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     }
 }
 
-// A parked game's envs read zero: obs rows, and (bound) mask / source rows.
+// A parked game's envs read zero: mask / source rows (when p.mask is set), and
+// obs rows (zero_outputs).
+template <int NT>
+__device__ __forceinline__ void zero_mask_rows(const EngineParams& p, const Game& G) {
+    if (!p.mask) return;
+    const size_t n = (size_t)G.nviews * p.HW;
+    int32_t* m = p.mask + (size_t)G.env0 * p.HW * MRTS_MASK_CH;
+    for (size_t i = threadIdx.x; i < n * MRTS_MASK_CH; i += NT) m[i] = 0;
+    for (size_t i = threadIdx.x; i < n; i += NT) p.src_out[(size_t)G.env0 * p.HW + i] = 0;
+}
 template <int NT, int P, typename OT>
 __device__ __forceinline__ void zero_outputs(const EngineParams& p, const Game& G) {
     const size_t n = (size_t)G.nviews * p.HW;
     OT* obs = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * p.HW * P;
     for (size_t i = threadIdx.x; i < n * P; i += NT) obs[i] = (OT)0;
-    if (p.mask) {
-        int32_t* m = p.mask + (size_t)G.env0 * p.HW * MRTS_MASK_CH;
-        for (size_t i = threadIdx.x; i < n * MRTS_MASK_CH; i += NT) m[i] = 0;
-        for (size_t i = threadIdx.x; i < n; i += NT) p.src_out[(size_t)G.env0 * p.HW + i] = 0;
-    }
+    zero_mask_rows<NT>(p, G);
 }
 
 // ---------------------------------------------------------------------------
@@ -407,10 +450,14 @@ __global__ __launch_bounds__(NT) void k_raw(EngineParams p, int32_t* raw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds L = carve(smem, p.HW, p.W, NT);
     const int g = blockIdx.x, HW = p.HW;
-    if (game_parked(p, g)) return;
-    load_game<NT>(p, L, g);
     const Game G = game_of(p, g);
     const int PR = p.partial_obs ? 7 : 6, nw = HW / 32 + 1;
+    if (game_parked(p, g)) {   // a parked game's envs read zero (mrts_park_games)
+        int32_t* out = raw + (size_t)G.env0 * PR * HW;
+        for (int i = threadIdx.x; i < G.nviews * PR * HW; i += NT) out[i] = 0;
+        return;
+    }
+    load_game<NT>(p, L, g);
     if (p.partial_obs) compute_vis<NT>(p, L);
     for (int v = 0; v < G.nviews; v++) {
         int32_t* out = raw + (size_t)(G.env0 + v) * PR * HW;
@@ -436,7 +483,10 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds L = carve(smem, p.HW, p.W, NT);
     const int g = blockIdx.x;
-    if (game_parked(p, g)) return;   // its rows were zeroed when it was parked
+    if (game_parked(p, g)) {   // the caller's buffers need not be the ones zeroed at park time
+        zero_mask_rows<NT>(p, game_of(p, g));
+        return;
+    }
     load_game<NT>(p, L, g);
     emit_outputs<NT, 29, int32_t>(p, L, game_of(p, g), false, true);
 }
@@ -725,7 +775,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
     if (FB) L.outw = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
-    int* const early_cnt = reinterpret_cast<int*>(smem + fb_tail_offset(HW, p.W, NT) + a16(bots::bot_tail_bytes(HW, p.W)));
+    int* const early_cnt = reinterpret_cast<int*>(smem + fb_early_cnt_offset(HW, p.W, NT));
     if (FB && threadIdx.x == 0) *early_cnt = 0;   // read after several barriers below
     // issue priority: the game logic (latency-bound chains of LDS steps and
     // barriers) over other workgroups' output streams (memory-bound), which
@@ -1023,7 +1073,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // + getMasks of the next tick (bound mask outputs): every read of this
     //   game's source rows (phase 1) is behind the barriers above
     const bool botg = FB && g >= p.nsp_games && NT > 64;
-    if (FB && P == 29 && botg) {
+    if (FB && P == 29 && botg && p.early_bot) {
         // Early bot (full observability: the bot writes none of the arrays phase A
         // reads -- unit / act / wall stay as stored, the step's scalars and
         // visibility words are left alone, its small arrays go to the tail region):
@@ -1033,7 +1083,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         __syncthreads();
         if (threadIdx.x < 64) {
             __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
-            bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT));
+            bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT), L.wall);
         }
         else
             emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, 64, early_cnt);
@@ -1409,6 +1459,10 @@ hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, in
     hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->HW, p->map_wall + (size_t)map * p->HW,
                        p->W, p->H, size, rgb);
     return hipGetLastError();
+}
+int mrts_engine_early_bot_ok(int HW, int W) {
+    const int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
+    return NT > 64 && mrts::early_bot_disjoint(HW, W, NT) ? 1 : 0;
 }
 size_t mrts_engine_fused_lds_bytes(int HW, int W) {
     const int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;

@@ -7,15 +7,25 @@ Java (JNIGridnetVecClient over JPype) and in the per-env numpy loops
 (_encode_obs, action packing, reward weighting) happens in libmicrorts_amd.so
 kernels on the GPU; this class only moves buffers and keeps the Python contract.
 
-Return types
-  * default (return_tensors=False): exactly the reference's -- numpy int32 obs
+Return types (`return_tensors`, or the environment variable MICRORTS_AMD_RETURN
+when the keyword is not given -- so an unmodified driver script can select one)
+  * "numpy" (False, the default): exactly the reference's -- numpy int32 obs
     (N,H,W,29), numpy int32 masks (N,H*W,78), numpy float64 rewards, numpy bool
     dones, a list of {"raw_rewards": row} dicts.
-  * return_tensors=True: device-resident torch tensors (obs float32 by default,
+  * "tensors" (True): device-resident torch tensors (obs float32 by default,
     masks int32, rewards float64, dones bool) and a lazily materialised infos
     sequence.  Tensors alias engine-owned buffers that are overwritten by the
     next call (the ownership rule of the reference's shared-memory env,
     vec_env.py:1331-1362).
+  * "hybrid": the contract an unmodified experiments/ppo_gridnet.py needs to keep
+    obs and masks in HBM: obs (float32 device tensor: its
+    `torch.Tensor(x)` aliases a float32 tensor, ppo_gridnet.py:421, 476) and masks
+    (int32 device tensor: `torch.tensor(x).to(device)`, :466) stay on the GPU,
+    while rewards (numpy float64, `raw @ reward_weight` in numpy as the
+    reference), dones (numpy bool) and infos (a list of {"raw_rewards": numpy
+    row}) are host objects, because MicroRTSStatsRecorder indexes dones[i] /
+    infos[i] per env and VecMonitor accumulates with numpy (:138-160).  Host
+    actions (:475) are accepted as in the numpy contract.
 """
 import json
 import os
@@ -128,6 +138,20 @@ class HostArrayPool:
         return out.numpy()
 
 
+CONTRACTS = {False: "numpy", "numpy": "numpy", True: "tensors", "tensors": "tensors", "hybrid": "hybrid"}
+
+
+def contract_of(return_tensors):
+    """The return contract for a `return_tensors` keyword value; None = the
+    environment variable MICRORTS_AMD_RETURN (numpy | tensors | hybrid), default numpy."""
+    if return_tensors is None:
+        return_tensors = os.environ.get("MICRORTS_AMD_RETURN", "numpy").strip().lower() or "numpy"
+    try:
+        return CONTRACTS[return_tensors]
+    except (KeyError, TypeError):
+        raise ValueError(f"return_tensors must be one of False / True / 'numpy' / 'tensors' / 'hybrid', got {return_tensors!r}")
+
+
 class MicroRTSGridModeVecEnv:
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 150}
     _cycle_min = 0   # map cycling when len(cycle_maps) > _cycle_min (vec_env.py:1038)
@@ -169,7 +193,7 @@ class MicroRTSGridModeVecEnv:
         graph_triples_file="triples.tsv",
         *,
         device=None,
-        return_tensors=False,
+        return_tensors=None,
         obs_dtype=None,
         eager_masks=True,
         bot_fusion=True,
@@ -239,9 +263,11 @@ class MicroRTSGridModeVecEnv:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise MicroRTSError(f"device must be a HIP/cuda device, got {self.device}")
-        self.return_tensors = return_tensors
+        self.contract = contract_of(return_tensors)
+        self.return_tensors = self.contract == "tensors"
+        self._host_outputs = self.contract == "numpy"   # obs / masks copied to numpy
         if obs_dtype is None:
-            obs_dtype = torch.float32 if return_tensors else torch.int32
+            obs_dtype = torch.int32 if self._host_outputs else torch.float32
         if obs_dtype not in (torch.float32, torch.int32):
             raise ValueError("obs_dtype must be torch.float32 or torch.int32")
         self.obs_dtype = obs_dtype
@@ -301,7 +327,8 @@ class MicroRTSGridModeVecEnv:
         self.source_unit_idxs = self.source_unit_idxs.reshape((self.source_unit_idxs.shape + (1,)))
         self._mask_fresh = False   # _mask / _src hold getMasks(0) of the current state
         self._pool = None          # numpy contract: page-locked output arrays (HostArrayPool)
-        self._act_stage = None     # numpy contract: page-locked int64 staging of the host actions
+        self._act_stage = None     # host actions: page-locked int64 staging buffer
+        self._act_copied = None    # event after the staging buffer's last H2D copy (reused only once it fired)
         # optional {kernel name: [(start, end) torch.cuda.Event]} filled around
         # each engine launch on the launch stream (bench.py roofline timing)
         self.kernel_events = None
@@ -347,7 +374,7 @@ class MicroRTSGridModeVecEnv:
         torch.cuda.current_stream(self.device).synchronize()
 
     def _obs_out(self):
-        if self.return_tensors:
+        if not self._host_outputs:
             return self._obs
         obs = self._host("obs", self._obs)
         self._sync()
@@ -367,7 +394,7 @@ class MicroRTSGridModeVecEnv:
             self._launch("get_masks", _native.lib().mrts_get_masks, self._h, self._stream(), self._mask.data_ptr(),
                          self._src.data_ptr())
             self._mask_fresh = True
-        if self.return_tensors:
+        if not self._host_outputs:
             return self._mask
         mask = self._host("mask", self._mask)
         self._sync()
@@ -375,7 +402,7 @@ class MicroRTSGridModeVecEnv:
 
     @property
     def source_unit_mask(self):
-        return self._src if self.return_tensors else self._src.cpu().numpy()
+        return self._src.cpu().numpy() if self._host_outputs else self._src
 
     def step_async(self, actions):
         """vec_env.py:968-984: actions (N, H*W*7) (or any shape with N*H*W*7 elements)."""
@@ -390,10 +417,16 @@ class MicroRTSGridModeVecEnv:
             a = np.asarray(actions).reshape(self.num_envs, hw, 7)
             if self._act_stage is None:
                 self._act_stage = torch.empty(tuple(self._actions.shape), dtype=torch.int64, pin_memory=True)
+                self._act_copied = torch.cuda.Event()
+            else:
+                # the previous step's DMA may still be queued (the tensor contract
+                # never syncs the stream): the staging buffer is rewritten only after it
+                self._act_copied.synchronize()
             # one host pass into page-locked memory, then a DMA at full PCIe rate (a
             # pageable source would be staged by the runtime in small chunks)
             np.copyto(self._act_stage.numpy(), a, casting="unsafe")
             self._actions.copy_(self._act_stage, non_blocking=True)
+            self._act_copied.record(torch.cuda.current_stream(self.device))
         self._actions_in = self._actions
 
     def step_wait(self):
@@ -421,7 +454,8 @@ class MicroRTSGridModeVecEnv:
         reward = self._host("raw", self._raw)
         done = self._host("done", self._done)
         cycling = len(self.cycle_maps) > self._cycle_min
-        if not cycling:   # one stream sync for every output
+        obs = self._obs   # hybrid contract: obs stay in HBM
+        if not cycling and self._host_outputs:   # one stream sync for every output
             obs = self._host("obs", self._obs)
         self._sync()
         done = done.astype(bool)
@@ -429,8 +463,9 @@ class MicroRTSGridModeVecEnv:
             reward[:, 1:] = 0
         if cycling:
             self._cycle(done[:, 0])
-            obs = self._host("obs", self._obs)
-            self._sync()
+            if self._host_outputs:
+                obs = self._host("obs", self._obs)
+                self._sync()
         infos = [{"raw_rewards": item} for item in reward]
         return obs, reward @ self.reward_weight, done[:, 0], infos
 
@@ -574,7 +609,7 @@ class MicroRTSBotVecEnv(MicroRTSGridModeVecEnv):
             map_paths = [map_paths]
         super().__init__(num_selfplay_envs=0, num_bot_envs=len(ai1s), partial_obs=partial_obs, max_steps=max_steps,
                          render_theme=render_theme, ai2s=ai2s, map_paths=map_paths, reward_weight=reward_weight,
-                         device=device, eager_masks=False, _ai1s=ai1s)
+                         device=device, eager_masks=False, return_tensors=False, _ai1s=ai1s)
         self.ai1s = ai1s
         self.observation_space = Discrete(2)
         self.action_space = Discrete(2)

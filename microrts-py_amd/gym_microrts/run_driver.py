@@ -1,6 +1,11 @@
 """Run a reference driver script unmodified on the MI355X engine.
 
-    python -m gym_microrts.run_driver experiments/ppo_gridnet.py --num-selfplay-envs 24 ...
+    python -m gym_microrts.run_driver [--contract numpy|tensors|hybrid] experiments/ppo_gridnet.py --num-selfplay-envs 24 ...
+
+`--contract hybrid` (the same as MICRORTS_AMD_RETURN=hybrid in the environment)
+gives every MicroRTSGridModeVecEnv the script constructs the zero-copy contract an
+unmodified ppo_gridnet.py can consume: obs / masks stay device tensors, rewards /
+dones / infos are numpy (gym_microrts/envs/vec_env.py module docstring).
 
 The reference's drivers (experiments/ppo_gridnet.py:17-23, ppo_gridnet_eval.py,
 hello_world.py) import `gym.spaces`, `stable_baselines3.common.vec_env` and
@@ -57,6 +62,18 @@ def main(argv=None):
     if not argv or argv[0] in ("-h", "--help"):
         print(__doc__)
         return 0
+    if argv[0].startswith("--contract"):
+        if "=" in argv[0]:
+            contract, argv = argv[0].split("=", 1)[1], argv[1:]
+        else:
+            contract, argv = argv[1], argv[2:]
+        if contract not in ("numpy", "tensors", "hybrid"):
+            print(f"unknown contract {contract!r}: numpy | tensors | hybrid", file=sys.stderr)
+            return 2
+        os.environ["MICRORTS_AMD_RETURN"] = contract
+    if not argv:
+        print(__doc__)
+        return 2
     script = argv[0]
     used = install()
     if used:

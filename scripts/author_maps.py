@@ -114,6 +114,15 @@ def main():
     # 40 barracks for player 0 (issue()'s pending-produce candidates beyond 16)
     field = [("Barracks", 0, x, y, 0, 4) for y in (1, 4, 7, 10, 13) for x in range(0, 16, 2)]
     write_map("16x16/barracksField16x16.xml", 16, 16, field + [B(1, 15, 15), W(1, 15, 14)], res=(40, 5))
+    # walled maps whose cell count is not a multiple of 4 (the fused k_step's early bot
+    # reads the step's terrain in place there: VERDICT r2 item 1); any size is legal
+    # (PCG/pcg.py:9-10 draws width and height freely), the terrain format is PCG/maps/wall-1
+    write_map("15x15/basesWorkersWalls15x15.xml", 15, 15,
+              [R(0, 0), R(0, 1), R(14, 14), R(14, 13), B(0, 2, 2), B(1, 12, 12), W(0, 1, 1), W(1, 13, 13)],
+              walls=[(7, 5), (7, 6), (7, 8), (7, 9), (5, 7), (6, 7), (8, 7), (9, 7), (4, 2), (4, 3), (10, 12), (10, 11)])
+    write_map("9x13/basesWorkersWalls9x13.xml", 9, 13,
+              [R(0, 0), R(0, 1), R(8, 12), R(8, 11), B(0, 2, 2), B(1, 6, 10), W(0, 1, 1), W(1, 7, 11)],
+              walls=[(1, 6), (2, 6), (3, 6), (5, 6), (6, 6), (7, 6), (4, 3), (4, 9)])
     # barricades: wall at (6,6) pinned, the rest authored (point symmetric)
     walls = []
     for k in range(6, 10):

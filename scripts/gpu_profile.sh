@@ -1,23 +1,34 @@
 #!/bin/bash
-# One gpurun call: GPU parity tests, the bench line, a rocprofv3 kernel-trace
-# summary of the same bench command, and separate PMC passes for HBM bytes
-# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
+# One gpurun call at a build: the -m gpu suite, the bench line, rocprofv3
+# kernel-trace summaries and separate PMC passes (FETCH_SIZE and WRITE_SIZE cannot
+# share a pass on gfx950) of the headline and of configs[1] (1024 envs vs device
+# coacAI).  The PMC summary is stamped with the library's sha256 and copied to
+# profiles/pmc_latest.json on the box, so the final bench lines carry traffic.
 #   /usr/local/graft/bin/gpurun --timeout 1200 -- bash scripts/gpu_profile.sh TAG
+#   SKIP_TESTS=1 to skip the suite.
 set -euo pipefail
 TAG=${1:-run}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p "$O"
-BENCH="bench.py --steps 100 --warmup 20 --no-cpu-baseline"
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 400 python -m pytest tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 \
+    || { echo "pytest failed"; tail -40 "$O/pytest_gpu.log"; exit 1; }
+  tail -2 "$O/pytest_gpu.log"
 fi
-timeout -k 10 300 python bench.py > "$O/bench.json" 2> "$O/bench.err"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt" -o kt -- python3 $BENCH > "$O/bench_kt.json" 2> "$O/kt.err"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$O/fetch" -o fetch -- python3 $BENCH --no-kernel-events > "$O/bench_fetch.json" 2> "$O/fetch.err"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$O/write" -o write -- python3 $BENCH --no-kernel-events > "$O/bench_write.json" 2> "$O/write.err"
-# configs[1] (1024 envs vs device coacAI): the kernel trace of its bench command too
+BENCH="bench.py --steps 100 --warmup 20 --no-cpu-baseline"
 COAC="bench.py --workload coac --envs-per-gpu 1024 --steps 300 --warmup 20 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt" -o kt -- python3 $BENCH > "$O/bench_kt.json" 2> "$O/kt.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt_coac" -o kt -- python3 $COAC > "$O/bench_coac_kt.json" 2> "$O/kt_coac.err"
+for W in selfplay coac; do
+  if [ $W = selfplay ]; then CMD="$BENCH"; KEY=selfplay@8192; else CMD="$COAC"; KEY=coac@1024; fi
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$O/pmc_$W/fetch" -o fetch -- python3 $CMD --no-kernel-events > "$O/pmc_$W.fetch.json" 2> "$O/pmc_$W.fetch.err"
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$O/pmc_$W/write" -o write -- python3 $CMD --no-kernel-events > "$O/pmc_$W.write.json" 2> "$O/pmc_$W.write.err"
+  python3 scripts/pmc_summary.py "$O/pmc_$W" "$O/pmc_latest.json" --workload $KEY --command "$CMD" > "$O/pmc_$W.txt"
+done
+cp "$O/pmc_latest.json" profiles/pmc_latest.json
+timeout -k 10 300 python bench.py > "$O/bench.json" 2> "$O/bench.err"
+timeout -k 10 300 python bench.py --workload coac --envs-per-gpu 1024 --no-cpu-baseline > "$O/bench_coac.json" 2> "$O/bench_coac.err"
+cat "$O/bench.json" "$O/bench_coac.json"
 echo done > "$O/DONE"

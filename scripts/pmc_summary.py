@@ -1,25 +1,44 @@
 """Summarise rocprofv3 PMC passes into per-kernel HBM bytes per launch.
 
-  python scripts/pmc_summary.py gpurun_out/TAG profiles/TAG_pmc.json
+  python scripts/pmc_summary.py gpurun_out/TAG/pmc_selfplay profiles/pmc_latest.json \
+      --workload selfplay@8192 [--lib microrts-py_amd/gym_microrts/libmicrorts_amd.so]
 
-Reads TAG/fetch/*_counter_collection.csv (FETCH_SIZE) and
-TAG/write/*_counter_collection.csv (WRITE_SIZE), one pass each (they cannot
+Reads SRC/fetch/*_counter_collection.csv (FETCH_SIZE) and
+SRC/write/*_counter_collection.csv (WRITE_SIZE), one pass each (they cannot
 share a pass on gfx950).  Corrections from MI355X_MICROARCH.md "HBM":
 rocprofv3 reports both counters in KiB; on gfx950 FETCH_SIZE counts exactly half
 the bytes of wide (16 B/lane) coalesced streaming reads, so it is doubled;
 WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Kernels whose loads
 are narrower than 16 B/lane are flagged "uncalibrated" (the doubling may not
 apply to them).
+
+The summary is stamped with the sha256 of the library the passes ran
+(`_meta.lib_sha256`) and filed under the bench workload it measured
+(`workloads[<workload>@<envs>]`); entries for other workloads of the same build
+are kept, a different build starts the file afresh.  bench.py reports
+`roofline.traffic` only when the stamp matches the library it runs.
 """
+import argparse
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
-import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "microrts-py_amd", "gym_microrts", "libmicrorts_amd.so")
 
 # kernels whose global loads are 16 B/lane (dwordx4) streaming reads
 WIDE_LOAD_KERNELS = ("k_masks", "k_step", "k_reset", "k_sample")
+
+
+def sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 def short(name):
@@ -36,7 +55,7 @@ def read(pattern, counter):
     return out
 
 
-def main(src, dst):
+def summarise(src):
     fetch = read(os.path.join(src, "fetch", "*_counter_collection.csv"), "FETCH_SIZE")
     write = read(os.path.join(src, "write", "*_counter_collection.csv"), "WRITE_SIZE")
     res = {}
@@ -50,10 +69,34 @@ def main(src, dst):
         res[k] = {"fetch_bytes_raw": f, "fetch_bytes": fc, "write_bytes": w,
                   "hbm_bytes": None if fc is None or w is None else fc + w,
                   "launches": len(fetch.get(k, [])), "fetch_correction": "x2 (gfx950, 16B/lane)" if wide else "uncalibrated"}
-    json.dump(res, open(dst, "w"), indent=1)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--workload", required=True, help="bench workload key, <workload>@<envs per gpu>")
+    ap.add_argument("--lib", default=LIB)
+    ap.add_argument("--command", default="")
+    a = ap.parse_args()
+    res = summarise(a.src)
+    digest = sha256(a.lib)
+    doc = {}
+    if os.path.exists(a.dst):
+        try:
+            doc = json.load(open(a.dst))
+        except ValueError:
+            doc = {}
+    if doc.get("_meta", {}).get("lib_sha256") != digest:
+        doc = {}
+    doc.setdefault("_meta", {"lib_sha256": digest, "lib": os.path.relpath(a.lib, REPO),
+                             "counters": "FETCH_SIZE x2 (gfx950 16 B/lane) + WRITE_SIZE, KiB -> bytes, separate passes"})
+    doc.setdefault("workloads", {})[a.workload] = {"command": a.command, "kernels": res}
+    json.dump(doc, open(a.dst, "w"), indent=1)
     for k, v in res.items():
-        print(k, {a: (round(b / 1e6, 2) if isinstance(b, float) else b) for a, b in v.items()})
+        print(a.workload, k, {x: (round(y / 1e6, 2) if isinstance(y, float) else y) for x, y in v.items()})
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main()

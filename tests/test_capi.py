@@ -110,3 +110,25 @@ def test_env_requires_gpu_when_absent():
 
     with pytest.raises(RuntimeError, match="GPU"):
         MicroRTSGridModeVecEnv(num_selfplay_envs=2, num_bot_envs=0, map_paths=["maps/16x16/basesWorkers16x16.xml"])
+
+
+def test_fused_early_bot_layout_is_race_free_for_every_size():
+    """the bot-fused k_step's early bot (wave 0) runs beside
+    emit_outputs' phase A (waves 1..).  For every map size the engine fuses (W <= 32,
+    H <= 64, H*W > 64, LDS within 160 KB) the bot's LDS writes must miss phase A's
+    reads (unit / act / wall / scalars) and phase A's writes (output words, counter)
+    must miss everything the bot touches -- in particular on sizes whose cell count
+    is not a multiple of 4, where the bot's own wall slot lands inside the step's
+    terrain (the bot now reads the step's terrain in place).  Checked by the
+    library from the two LDS carves the kernels use."""
+    from gym_microrts import _native
+
+    f = _native.lib().mrts_fused_layout_ok
+    fusable = [(w, h) for w in range(1, 33) for h in range(1, 65) if f(w, h) >= 0]
+    assert len(fusable) > 1500
+    assert all(w * h > 64 for w, h in fusable)
+    bad = [(w, h) for w, h in fusable if f(w, h) != 1]
+    assert not bad, bad[:20]
+    odd = [(w, h) for w, h in fusable if (w * h) % 4]
+    assert (15, 15) in odd and (9, 13) in odd
+    assert f(8, 8) == -1 and f(33, 16) == -1 and f(0, 5) == -1

@@ -210,3 +210,34 @@ def test_ppo_gridnet_wrapper_stack_on_device(compat, tmp_path):
     assert all(l <= max_steps for _, l in episodes)
     assert base.error_flags() == 0
     envs.close()
+
+
+def test_return_contract_from_environment(monkeypatch):
+    """MICRORTS_AMD_RETURN selects the return contract of an env constructed without
+    `return_tensors` (an unmodified ppo_gridnet.py); the keyword wins when given."""
+    from gym_microrts.envs.vec_env import contract_of
+
+    monkeypatch.delenv("MICRORTS_AMD_RETURN", raising=False)
+    assert contract_of(None) == "numpy"
+    monkeypatch.setenv("MICRORTS_AMD_RETURN", "hybrid")
+    assert contract_of(None) == "hybrid"
+    assert contract_of(False) == "numpy" and contract_of(True) == "tensors" and contract_of("hybrid") == "hybrid"
+    monkeypatch.setenv("MICRORTS_AMD_RETURN", "bogus")
+    with pytest.raises(ValueError):
+        contract_of(None)
+
+
+def test_run_driver_contract_flag(tmp_path, monkeypatch):
+    """`run_driver --contract hybrid script.py` exports MICRORTS_AMD_RETURN before the
+    script runs, so the script itself is not edited."""
+    from gym_microrts import run_driver
+
+    out = tmp_path / "seen.txt"
+    script = tmp_path / "probe.py"
+    script.write_text(f"import os\nopen({str(out)!r}, 'w').write(os.environ.get('MICRORTS_AMD_RETURN', ''))\n")
+    monkeypatch.delenv("MICRORTS_AMD_RETURN", raising=False)
+    assert run_driver.main(["--contract", "hybrid", str(script)]) == 0
+    assert out.read_text() == "hybrid"
+    assert run_driver.main(["--contract=tensors", str(script)]) == 0
+    assert out.read_text() == "tensors"
+    assert run_driver.main(["--contract", "nope", str(script)]) == 2

@@ -69,9 +69,14 @@ def test_bot_lockstep_16x16(ai, partial_obs):
 
 @pytest.mark.parametrize("map_path", ["maps/8x8/basesWorkers8x8.xml", "maps/10x10/basesTwoWorkers10x10.xml",
                                       "maps/24x24/basesWorkers24x24.xml", "maps/barricades24x24.xml",
-                                      "maps/4x4/baseTwoWorkers4x4.xml", "maps/32x32/basesWorkers32x32.xml"])
+                                      "maps/4x4/baseTwoWorkers4x4.xml", "maps/32x32/basesWorkers32x32.xml",
+                                      "maps/15x15/basesWorkersWalls15x15.xml", "maps/9x13/basesWorkersWalls9x13.xml"])
 def test_mixed_bots_lockstep_other_maps(map_path):
-    """... including 32x32, whose bot-fused k_step needs > 64 KB of LDS"""
+    """... including 32x32, whose bot-fused k_step needs > 64 KB of LDS,
+    and walled maps whose cell count is not a multiple of 4 (225, 117), full
+    observability and fusion on: the fused early bot reads the step's terrain in
+    place while the other waves build the terrain plane and move masks from it
+    (wall plane /root/reference/tests/test_observation.py:86-108)"""
     ais = (BOTS * 3)[:16] + ["passiveAI"] * 2
     lockstep(ais, map_path, 4, 500, max_steps=300)
 
