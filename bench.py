@@ -329,6 +329,7 @@ def run_gpu(args, rank, world, local_rank):
               reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev, **extra)
     hw = env.height * env.width
     act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
+    act_host = torch.empty((n, hw, 7), dtype=torch.int64, pin_memory=True) if args.api != "tensor" else None
     lib = _native.lib()
     seed = args.seed   # one stream over global env indices: rank r samples envs [env0, env0 + n)
     ev = {}
@@ -348,7 +349,12 @@ def run_gpu(args, rank, world, local_rank):
             env.kernel_events.setdefault("sample", []).append((e0, e1))
         _native.check(rc, None, "sample")
         if args.api != "tensor":   # ppo_gridnet.py:475: host int64 actions (N, HW*7)
-            return env.step(act.cpu().numpy().reshape(n, -1))
+            # the stand-in policy's action.cpu(): into a page-locked buffer (the driver's
+            # choice; a fresh pageable array would add first-touch faults + a staged copy
+            # that are the driver's cost, not the env's), synchronous like .cpu()
+            act_host.copy_(act, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return env.step(act_host.numpy().reshape(n, -1))
         return env.step(act)
 
     timing = [False]

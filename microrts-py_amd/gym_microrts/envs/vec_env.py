@@ -329,6 +329,9 @@ class MicroRTSGridModeVecEnv:
         self._pool = None          # numpy contract: page-locked output arrays (HostArrayPool)
         self._act_stage = None     # host actions: page-locked int64 staging buffer
         self._act_copied = None    # event after the staging buffer's last H2D copy (reused only once it fired)
+        self._act_src = None       # a caller's page-locked action array being copied (kept alive until step_wait's sync)
+        self._mask_prefetch = None # numpy contract: host masks of the current state, copied in step_wait's sync
+        self._mask_wanted = False  # get_action_mask() was called since the last step (the rollout loop's pattern)
         # optional {kernel name: [(start, end) torch.cuda.Event]} filled around
         # each engine launch on the launch stream (bench.py roofline timing)
         self.kernel_events = None
@@ -383,6 +386,7 @@ class MicroRTSGridModeVecEnv:
     # ------------------------------------------------------------------- API
     def reset(self):
         """vec_env.py:278-282"""
+        self._mask_prefetch = None
         _native.check(_native.lib().mrts_reset(self._h, self._stream(), self._obs.data_ptr()), self._h, "reset")
         self._mask_fresh = self.eager_masks
         return self._obs_out()
@@ -396,6 +400,10 @@ class MicroRTSGridModeVecEnv:
             self._mask_fresh = True
         if not self._host_outputs:
             return self._mask
+        self._mask_wanted = True
+        if self._mask_prefetch is not None:   # copied behind the obs in the last step_wait's one sync
+            mask, self._mask_prefetch = self._mask_prefetch, None
+            return mask
         mask = self._host("mask", self._mask)
         self._sync()
         return mask
@@ -414,7 +422,19 @@ class MicroRTSGridModeVecEnv:
                 return
             self._actions.copy_(a)
         else:
-            a = np.asarray(actions).reshape(self.num_envs, hw, 7)
+            a = np.asarray(actions)
+            if self.contract != "tensors" and a.dtype == np.int64 and a.size == self._actions.numel() and a.flags.c_contiguous:
+                t = torch.from_numpy(a.reshape(-1))
+                if t.is_pinned():
+                    # the caller's array is page-locked already (e.g. a view of a pinned
+                    # tensor the policy copied its actions into): one DMA straight from it,
+                    # no host pass.  step_wait syncs the stream before returning (numpy /
+                    # hybrid contracts), so the array is free again once step() returns.
+                    self._actions.view(-1).copy_(t, non_blocking=True)
+                    self._act_src = t
+                    self._actions_in = self._actions
+                    return
+            a = a.reshape(self.num_envs, hw, 7)
             if self._act_stage is None:
                 self._act_stage = torch.empty(tuple(self._actions.shape), dtype=torch.int64, pin_memory=True)
                 self._act_copied = torch.cuda.Event()
@@ -451,13 +471,22 @@ class MicroRTSGridModeVecEnv:
             return self._obs, self._rew, self._done0, LazyInfos(raw)
         self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
                      self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
+        self._mask_prefetch = None
+        # numpy contract + eager masks, when the caller reads the masks every step (the
+        # rollout loop does: ppo_gridnet.py:466): the next get_action_mask()'s host copy
+        # rides behind the obs copy, in this call's one sync
+        prefetch = self._host_outputs and self.eager_masks and self._mask_wanted
+        self._mask_wanted = False
         reward = self._host("raw", self._raw)
         done = self._host("done", self._done)
         cycling = len(self.cycle_maps) > self._cycle_min
         obs = self._obs   # hybrid contract: obs stay in HBM
         if not cycling and self._host_outputs:   # one stream sync for every output
             obs = self._host("obs", self._obs)
+            if prefetch:
+                self._mask_prefetch = self._host("mask", self._mask)
         self._sync()
+        self._act_src = None
         done = done.astype(bool)
         if not self.reward_shaping:
             reward[:, 1:] = 0
@@ -465,6 +494,8 @@ class MicroRTSGridModeVecEnv:
             self._cycle(done[:, 0])
             if self._host_outputs:
                 obs = self._host("obs", self._obs)
+                if prefetch:
+                    self._mask_prefetch = self._host("mask", self._mask)
                 self._sync()
         infos = [{"raw_rewards": item} for item in reward]
         return obs, reward @ self.reward_weight, done[:, 0], infos
@@ -483,6 +514,7 @@ class MicroRTSGridModeVecEnv:
         games = [int(g) for g in games]
         if not games:
             return
+        self._mask_prefetch = None
         maps = [self._game_map[g] for g in games] if maps is None else [int(m) for m in maps]
         for g, m in zip(games, maps):
             self._game_map[g] = m
@@ -501,6 +533,7 @@ class MicroRTSGridModeVecEnv:
         games = [int(g) for g in games]
         if not games:
             return
+        self._mask_prefetch = None
         ga = (ctypes.c_int32 * len(games))(*games)
         _native.check(_native.lib().mrts_park_games(self._h, self._stream(), ga, len(games), self._obs.data_ptr()), self._h,
                       "park_games")

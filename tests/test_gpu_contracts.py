@@ -96,3 +96,47 @@ def test_ppo_driver_configs3_4096(api):
                       log=lambda _: None)
     assert s["global_step"] == 4 * 4096 and s["finite"] and s["engine_error_flags"] == 0
     assert s["num_envs"] == 4096 and s["api"] == api
+
+
+@pytest.mark.parametrize("cycle", [False, True])
+def test_numpy_contract_pinned_actions_and_mask_prefetch(cycle):
+    """The numpy contract's fast paths change no byte: host
+    actions handed over in a page-locked array (one DMA, no staging pass) vs a
+    pageable one, masks copied behind the obs in step_wait's sync vs on demand;
+    a returned mask array is never overwritten by later calls."""
+    import torch
+
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+
+    m = "maps/16x16/basesWorkers16x16A.xml"
+    kw = dict(max_steps=25, map_paths=[m], reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), return_tensors=False,
+              cycle_maps=[m] if cycle else [])
+    ea = MicroRTSGridModeVecEnv(64, 0, **kw)
+    eb = MicroRTSGridModeVecEnv(64, 0, **kw)
+    et = MicroRTSGridModeVecEnv(64, 0, **dict(kw, return_tensors=True, obs_dtype=torch.int32))
+    np.testing.assert_array_equal(ea.reset(), eb.reset())
+    et.reset()
+    pinned = torch.empty((64, 256 * 7), dtype=torch.int64, pin_memory=True)
+    gen = torch.Generator(device=et.device)
+    gen.manual_seed(5)
+    kept = []
+    for s in range(60):
+        ma, mb = ea.get_action_mask(), eb.get_action_mask()
+        mt = et.get_action_mask()
+        np.testing.assert_array_equal(ma, mb)
+        np.testing.assert_array_equal(ma, mt.cpu().numpy())
+        kept.append((ma, ma.copy()))
+        a = _sample(mt, gen)
+        pinned.copy_(a.cpu())
+        oa, ra, da, ia = ea.step(pinned.numpy().copy())   # pageable: staging pass
+        ob, rb, db, ib = eb.step(pinned.numpy())          # page-locked: direct DMA
+        ot, rt, dt, it = et.step(a)
+        for x, y in ((oa, ob), (ra, rb), (da, db)):
+            np.testing.assert_array_equal(x, y, err_msg=f"step {s}")
+        np.testing.assert_array_equal(oa, ot.cpu().numpy())
+        np.testing.assert_array_equal(da, dt.cpu().numpy())
+    for arr, saved in kept:
+        np.testing.assert_array_equal(arr, saved)
+    for e in (ea, eb, et):
+        assert e.error_flags() == 0
+        e.close()

@@ -402,3 +402,35 @@ def test_reward_weight_reassigned_mid_run():
         _, rg, _, _ = g.step(torch.from_numpy(a).to(g.device))
         _, ro, _, _ = o.step(a)
         np.testing.assert_allclose(rg.cpu().numpy(), ro, rtol=0, atol=1e-12, err_msg=f"step {s}")
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_parked_games_read_zero_in_mask_and_raw_kernels(eager):
+    """a parked game's envs read zero from get_action_mask() (k_masks when
+    masks are not eager) and from the JNI-shaped raw observation (k_raw), whatever
+    those buffers held before the park -- not only the buffers bound at park time."""
+    torch = _torch()
+    from gym_microrts import _native
+
+    env = make_gpu_env(4, 2, os.path.join(MAPS, "maps/16x16/basesWorkers16x16.xml"), 2000, eager_masks=eager,
+                       return_tensors=True, obs_dtype=torch.int32)
+    env.reset()
+    hw = env.height * env.width
+    for s in range(5):
+        m = env.get_action_mask()
+        a = torch.zeros((env.num_envs, hw, 7), dtype=torch.int64, device=env.device)
+        env.step(a)
+    raw = torch.full((env.num_envs, 6, env.height, env.width), 7, dtype=torch.int32, device=env.device)
+    env._mask.fill_(3)
+    env._src.fill_(1)
+    env._mask_fresh = False
+    env.park_games([0, 3])   # envs 0, 1 (selfplay game 0) and 5 (bot game 3)
+    m = env.get_action_mask()
+    _native.check(_native.lib().mrts_get_raw_obs(env._h, env._stream(), raw.data_ptr()), env._h, "raw")
+    torch.cuda.synchronize()
+    parked, live = [0, 1, 5], [2, 3, 4]
+    assert int(m[parked].abs().sum()) == 0 and int(env._src[parked].abs().sum()) == 0
+    assert int(raw[parked].abs().sum()) == 0
+    assert int(env._src[live].sum()) > 0 and int(raw[live].sum()) > 0
+    assert int((m[live] == 3).sum()) == 0   # live rows rewritten by the mask kernel / eager masks
+    env.close()
