@@ -60,22 +60,22 @@ struct BL {   // LDS of one bot game
     uint32_t* pab;    // the PlayerAction's ResourceUsage positions + W, bits
     uint32_t* vis;    // cells observable by the bot's player (partial obs)
     uint8_t* wall;
-    int* sc;
+    int* sc;          // pending produce cost per player, error bits, [3] = units (workgroup setup)
+    uint32_t* fw;     // free-cell words (bot_fw_words)
 };
 
 __host__ __device__ inline size_t b16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t bot_lds_bytes(int HW, int W) {
-    const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
-    return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW) + b16((size_t)HW) + 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) +
-           b16(4 * 4);
-}
-
-// `tail`: where the small arrays (pend, pab, vis, sc) go when the caller keeps
+// free-cell words: two per 64 cells (one ballot) + a zero word past the last cell
+__host__ __device__ inline size_t bot_fw_words(int HW) { return (size_t)(HW + 63) / 64 * 2 + 1; }
+// `tail`: where the small arrays (pend, pab, vis, sc, fw) go when the caller keeps
 // them apart (the fused k_step's early bot, whose workgroup still reads the
 // step's scalars and visibility words while the bot runs); null = behind wall
 __host__ __device__ inline size_t bot_tail_bytes(int HW, int W) {
     const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
-    return 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) + b16(4 * 4);
+    return 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) + b16(4 * 4) + b16(4 * bot_fw_words(HW));
+}
+__host__ __device__ inline size_t bot_lds_bytes(int HW, int W) {
+    return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW) + b16((size_t)HW) + bot_tail_bytes(HW, W);
 }
 __host__ __device__ inline BL bot_carve(unsigned char* base, int HW, int W, unsigned char* tail = nullptr) {
     BL L;
@@ -97,7 +97,8 @@ __host__ __device__ inline BL bot_carve(unsigned char* base, int HW, int W, unsi
     L.pend = (uint32_t*)take(4 * posw);
     L.pab = (uint32_t*)take(4 * posw);
     L.vis = (uint32_t*)take(4 * ((size_t)HW / 32 + 1));
-    L.sc = (int*)take(4 * 4);   // pending produce cost per player, error bits
+    L.sc = (int*)take(4 * 4);   // pending produce cost per player, error bits, units
+    L.fw = (uint32_t*)take(4 * bot_fw_words(HW));
     return L;
 }
 
@@ -569,7 +570,65 @@ __device__ __forceinline__ int aa_execute(const BS& S, const BL& L, int4& a, int
 }
 
 // AbstractionLayerAI.translateActions (fillWithNones(gs, p, 1) is k_step's phase 3)
+// With the unit list and the abstract actions in registers (<= 64 each): whether
+// an entry is dropped (its unit or target gone, or completed) and whether its unit
+// is idle depend on the fixed state only, so every entry decides that in its own
+// lane (its unit's and its target's cells found in one pass over the list); only
+// the idle units' AbstractAction.execute, whose PlayerAction ResourceUsage grows
+// entry by entry, walks the entries in order; the kept entries are then written
+// back lane-parallel in their order.
+__device__ __forceinline__ void translate_actions_lanes(BS& S, const BL& L) {
+    const int lane = blane();
+    const bool valid = lane < S.naa;
+    int4 a = S.kA;
+    const int4 b = S.kB;
+    int cu = -1, tc = -1;
+    uint32_t act = 0;
+    for (int j = 0; j < S.n; j++) {   // uid -> cell of the entry's unit and of its target
+        const int uj = lane_value(S.kuid, j), cj = lane_value(S.kcell, j);
+        const uint32_t aj = (uint32_t)lane_value((int)S.kact, j);
+        if (uj == a.x) {
+            cu = cj;
+            act = aj;
+        }
+        if (uj == a.z) tc = cj;
+    }
+    bool done = false;   // aa_completed
+    switch (aa_kind(a)) {
+    case AA_MOVE: done = cu % S.W == pk_x(a.w) && cu / S.W == pk_y(a.w); break;
+    case AA_HARVEST:
+    case AA_ATTACK: done = tc < 0; break;
+    default: done = aa_done(a) != 0;
+    }
+    const bool keep = valid && cu >= 0 && !done;
+    unsigned long long ex = __ballot(keep && act == 0);
+    while (ex) {   // the idle units' execute, in LinkedHashMap order
+        const int k = __builtin_ctzll(ex);
+        ex &= ex - 1ull;
+        int4 ak = lane_int4(a, k);
+        const int4 bk = lane_int4(b, k);
+        const int cuk = lane_value(cu, k);
+        const int code = aa_execute(S, L, ak, bk, cuk);
+        if (code >= 0) {
+            RU r = usage(S, cuk, code, S.player);
+            if (consistent(S, r, L.pab, S.pa_res)) pa_add(S, L, cuk, code);
+        }
+        if (lane == k) a = ak;   // execute may mark it completed
+    }
+    const unsigned long long km = __ballot(keep);
+    if (keep) {
+        const int pos = __popcll(km & ((1ull << lane) - 1ull));
+        L.aa[2 * pos] = a;
+        L.aa[2 * pos + 1] = b;
+    }
+    S.naa = __popcll(km);   // (the register copy is stale from here on: only the LDS list is written back)
+}
+
 __device__ __forceinline__ void translate_actions(BS& S, const BL& L) {
+    if (S.n <= BT && S.naa <= BT) {
+        translate_actions_lanes(S, L);
+        return;
+    }
     int w = 0;
     const int n0 = S.naa;
     for (int k = 0; k < n0; k++) {
@@ -845,16 +904,18 @@ __device__ __forceinline__ void behaviours_parallel(BS& S, const BL& L, int army
     const unsigned long long own_workers = __ballot(own && ut_can_harvest(t));
     const int nworkers = __popcll(__ballot(own && t == WORKER)), nbases = __popcll(__ballot(own && t == BASE)),
               nbarracks = __popcll(__ballot(own && t == BARRACKS)), nf = __popcll(own_workers);
-    // this lane's existing abstract action (keys are unique)
+    // this lane's existing abstract action (keys are unique): its index from one
+    // scalar read per entry, then the entry itself gathered from that lane
     int ek = -1;
-    int4 ea = make_int4(0, 0, 0, 0), eb = make_int4(0, 0, 0, 0);
-    for (int j = 0; j < S.naa; j++) {   // (lane reads outside the divergent branch)
-        const int4 aj = lane_int4(S.kA, j), bj = lane_int4(S.kB, j);
-        if (own && aj.x == S.kuid && ek < 0) {
-            ek = j;
-            ea = aj;
-            eb = bj;
-        }
+    for (int j = 0; j < S.naa; j++)   // (lane reads outside the divergent branch)
+        if (ek < 0 && lane_value(S.kA.x, j) == S.kuid) ek = j;
+    if (!own) ek = -1;
+    const int es = max(ek, 0);
+    int4 ea = make_int4(lane_gather(S.kA.x, es), lane_gather(S.kA.y, es), lane_gather(S.kA.z, es), lane_gather(S.kA.w, es));
+    int4 eb = make_int4(lane_gather(S.kB.x, es), lane_gather(S.kB.y, es), lane_gather(S.kB.z, es), lane_gather(S.kB.w, es));
+    if (ek < 0) {
+        ea = make_int4(0, 0, 0, 0);
+        eb = make_int4(0, 0, 0, 0);
     }
     LaneDecision d{-1, make_int4(0, 0, 0, 0), make_int4(-1, 0, 0, 0), false};
     const int rank = __popcll(own_workers & ((1ull << lane) - 1ull));   // position among the player's workers
@@ -1158,7 +1219,7 @@ template <bool FUSED>
 __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem,
                                          const int32_t* step_sc = nullptr, bool pre_ok = false, int4 pre_aa = int4{0, 0, 0, 0},
                                          int4 pre_aa2 = int4{0, 0, 0, 0}, unsigned char* tail = nullptr,
-                                         const uint8_t* step_wall = nullptr) {
+                                         const uint8_t* step_wall = nullptr, bool preset = false) {
     const int g = p.nsp_games + b, lane = blane();
     const int HW = p.HW, W = p.W;
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
@@ -1198,7 +1259,10 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     // state it has just stored -- no reload.
     // Fused, its wall array too (wall_shared), and the first 128 abstract-action
     // words come prefetched in registers (pre_aa / pre_aa2: words lane, lane + 64).
-    for (int c = lane; c < HW; c += BT) {
+    // preset (the fused k_step's early bot, full observability): the workgroup has
+    // already built the pending reservations, the free-cell words and the unit list
+    // (mrts_engine.hip bot_setup_workgroup) and zeroed the tail arrays
+    for (int c = lane; !preset && c < HW; c += BT) {
         if (!FUSED) {
             int4 v = p.cells[(size_t)g * HW + c];
             L.unit[c] = (uint32_t)v.x;
@@ -1207,8 +1271,8 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         }
         if (!FUSED || (!step_wall && !wall_shared(HW))) L.wall[c] = p.map_wall[(size_t)map * HW + c];
     }
-    for (int i = lane; i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
-    for (int i = lane; i < visw; i += BT) L.vis[i] = 0;
+    for (int i = lane; !preset && i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
+    for (int i = lane; !preset && i < visw; i += BT) L.vis[i] = 0;
     {   // the abstract actions: the first 128 words come prefetched in registers when fused
         int i0 = 0;
         if (FUSED && pre_ok) {   // no global load is issued for them
@@ -1218,7 +1282,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         }
         for (int i = i0 + lane; i < 2 * S.naa; i += BT) L.aa[i] = aa_g[i];
     }
-    if (lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
+    if (!preset && lane < 3) L.sc[lane] = 0;   // pending produce cost per player, error bits
     bot_sync<FUSED>();
     // cells observable by the bot's player (PartiallyObservableGameState);
     // read only under partial observability (hidden units, PO* exploration)
@@ -1246,7 +1310,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         bot_sync<FUSED>();
     }
     // pending reservations of the visible units (isUnitActionAllowed)
-    for (int c = lane; c < HW; c += BT) {
+    for (int c = lane; !preset && c < HW; c += BT) {
         const uint32_t a = L.act[c];
         if (a == 0) continue;
         const int code = act_code(a), t = code_type(code);
@@ -1256,8 +1320,8 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         if (t == A_PRODUCE) atomicAdd(&L.sc[u_owner(L.unit[c])], u_owner(L.unit[c]) ? r.res[1] : r.res[0]);
     }
     // units in pgs.units order: ordered compaction by cell, then rank by uid
-    int n = 0;
-    for (int base = 0; base < HW; base += BT) {
+    int n = preset ? L.sc[3] : 0;
+    for (int base = 0; !preset && base < HW; base += BT) {
         const int c = base + lane;
         const bool has = c < HW && L.unit[c] != 0;
         const unsigned long long m = __ballot(has);
@@ -1265,7 +1329,8 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         n += __popcll(m);
     }
     bot_sync<FUSED>();
-    if (n <= BT) {   // rank by uid with the uids in registers (one per lane)
+    if (preset) {
+    } else if (n <= BT) {   // rank by uid with the uids in registers (one per lane)
         const int c = lane < n ? L.pa[lane] : 0, u = lane < n ? L.uid[c] : 0x7fffffff;
         int r = 0;
         for (int j = 0; j < n; j++) r += lane_value(u, j) < u;
@@ -1296,9 +1361,9 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     // free until the PlayerAction is built)
     S.rurow = 0;
     {
-        uint32_t* fw = reinterpret_cast<uint32_t*>(L.pa);
+        uint32_t* fw = L.fw;
         const int nwords = (HW + 63) / 64 * 2;
-        for (int base = 0; base < HW; base += BT) {
+        for (int base = 0; !preset && base < HW; base += BT) {
             const int c = base + lane;
             const unsigned long long m = __ballot(c < HW && !L.wall[c] && L.unit[c] == 0);
             if (lane == 0) {
@@ -1306,7 +1371,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
                 fw[base / 32 + 1] = (uint32_t)(m >> 32);
             }
         }
-        if (lane == 0) fw[nwords] = 0u;   // the row window's upper word past the last cell
+        if (!preset && lane == 0) fw[nwords] = 0u;   // the row window's upper word past the last cell
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         S.frow = 0;
         if (lane < p.H) {

@@ -357,12 +357,11 @@ static hipError_t upload_parked(mrts_vec *h, hipStream_t s) {
 static bool bound(mrts_vec *h) { return h && h->ws; }
 
 // Bot fusion applies to games whose bots play player 1 only (bot-vs-bot games
-// decide for both sides: separate k_bot), to maps whose step workgroup has
-// waves besides the bot's (H*W > 64, the 64-lane workgroup of mrts_engine.hip's
-// dispatch), and when both LDS regions fit a workgroup.
+// decide for both sides: separate k_bot), and when both LDS regions fit a
+// workgroup (the fused step workgroup has at least two waves: maps of <= 64
+// cells take 128 lanes, mrts_engine.hip step_nt).
 static bool fused(const mrts_vec *h) {
-    return h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && h->HW > 64 &&
-           mrts_engine_fused_lds_bytes(h->HW, h->W) <= 163840;
+    return h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && mrts_engine_fused_lds_bytes(h->HW, h->W) <= 163840;
 }
 
 // k_bot (when the tick's bot decisions are not already there) + k_step on s
@@ -625,7 +624,7 @@ int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {
 int mrts_fused_layout_ok(int32_t width, int32_t height) {
     if (width <= 0 || height <= 0 || width > 32 || height > 64) return -1;
     const int HW = width * height;
-    if (HW <= 64 || mrts_engine_fused_lds_bytes(HW, width) > 163840) return -1;
+    if (mrts_engine_fused_lds_bytes(HW, width) > 163840) return -1;
     return mrts_engine_early_bot_ok(HW, width);
 }
 

@@ -147,8 +147,9 @@ __host__ __device__ inline bool early_bot_disjoint(int HW, int W, int NT) {
     auto overlap = [&](const R& a, const R& b) { return lo(a) < lo(b) + b.n && lo(b) < lo(a) + a.n; };
     const size_t hw = (size_t)HW, posw = (size_t)(HW + 2 * W) / 32 + 1, visw = (size_t)HW / 32 + 1;
     if (B.unit != S.unit || B.uid != S.uid || B.act != S.act) return false;
-    const R bot_w[8] = {{B.ucell, 4 * hw}, {B.uuid, 4 * hw}, {B.pa, 4 * hw}, {B.aa, 32 * hw},
-                        {B.pend, 4 * posw}, {B.pab, 4 * posw}, {B.vis, 4 * visw}, {B.sc, 16}};
+    const R bot_w[9] = {{B.ucell, 4 * hw}, {B.uuid, 4 * hw}, {B.pa, 4 * hw}, {B.aa, 32 * hw},
+                        {B.pend, 4 * posw}, {B.pab, 4 * posw}, {B.vis, 4 * visw}, {B.sc, 16},
+                        {B.fw, 4 * bots::bot_fw_words(HW)}};
     const R bot_r[4] = {{B.unit, 4 * hw}, {B.uid, 4 * hw}, {B.act, 4 * hw}, {S.wall, hw}};
     const R a_r[4] = {{S.unit, 4 * hw}, {S.act, 4 * hw}, {S.wall, hw}, {S.sc, 4 * (size_t)SC_WORDS}};
     const R a_w[2] = {{z + fb_outw_offset(HW, W, NT), 32 * hw}, {z + fb_early_cnt_offset(HW, W, NT), 4}};
@@ -197,6 +198,60 @@ __device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsi
     }
     __syncthreads();
     return total;
+}
+
+// The early bot's setup, by the whole workgroup (all NT lanes, the state final
+// in LDS, before the waves split): the parts of bots::bot_game's setup that are
+// per cell -- the pending assignments' reservations and produce costs
+// (isUnitActionAllowed's ResourceUsage), the free-cell words of path finding, and
+// the unit list in pgs.units order (ordered compaction by cell, then ranks by uid)
+// -- into the bot's LDS arrays (its tail zeroed at the kernel's start); the bot
+// wave then starts at the abstract actions (bot_game, preset).  Full observability
+// only (the early path's condition), so the bot's view is the state itself.
+// `scratch`: the step's ballot words (compact_cells).
+template <int NT>
+__device__ __forceinline__ void bot_setup_workgroup(const EngineParams& p, unsigned char* smem, unsigned char* tail,
+                                                    const uint8_t* wall, unsigned long long* scratch) {
+    const int HW = p.HW, W = p.W, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const bots::BL B = bots::bot_carve(smem, HW, W, tail);
+    for (int base = 0; base < HW; base += NT) {
+        const int c = base + (int)threadIdx.x;
+        bool fr = false;
+        if (c < HW) {
+            const uint32_t u = B.unit[c], a = B.act[c];
+            fr = !wall[c] && u == 0;
+            if (a) {
+                const int code = act_code(a), t = code_type(code);
+                if (t == A_MOVE || t == A_PRODUCE) {
+                    const int d = code_param(code), pos = c + (d == 0 ? -W : d == 1 ? 1 : d == 2 ? W : -1) + W;
+                    atomicOr(&B.pend[pos >> 5], 1u << (pos & 31));
+                    if (t == A_PRODUCE && u_owner(u) >= 0) atomicAdd(&B.sc[u_owner(u)], ut_cost(code_utype(code)));
+                }
+            }
+        }
+        const unsigned long long m = __ballot(fr);   // cells base + 64 wv .. + 63
+        if (lane == 0 && base + 64 * wv < HW) {
+            B.fw[(base + 64 * wv) / 32] = (uint32_t)m;
+            B.fw[(base + 64 * wv) / 32 + 1] = (uint32_t)(m >> 32);
+        }
+    }
+    // unit list by cell (B.pa), its uids alongside (the first words of B.aa, rewritten by the bot later)
+    int32_t* const ucells = B.pa;
+    int32_t* const uids = reinterpret_cast<int32_t*>(B.aa);
+    const int n = compact_cells<NT>(HW, [&](int c) { return B.unit[c] != 0; }, ucells, scratch,
+                                    [&](int pos, int c) { uids[pos] = B.uid[c]; });
+    for (int i = threadIdx.x; i < n; i += NT) {   // rank by uid (uids are unique)
+        const int u = uids[i];
+        int r = 0, j = 0;
+        for (; j + 4 <= n; j += 4) {
+            const int4 v = *reinterpret_cast<const int4*>(uids + j);
+            r += (v.x < u) + (v.y < u) + (v.z < u) + (v.w < u);
+        }
+        for (; j < n; j++) r += uids[j] < u;
+        B.ucell[r] = ucells[i];
+        B.uuid[r] = u;
+    }
+    if (threadIdx.x == 0) B.sc[3] = n;
 }
 
 struct Game {
@@ -355,16 +410,16 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
         const int total = NV * HW * P;
         if (((HW * P) & 3) == 0) {   // every env's rows start 16-B aligned
             constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
+            // elements e .. e+3 are planes pl .. pl+3 of cell c, running on into cell
+            // c+1 past plane P-1: one paired LDS read (cells c, c+1) per 16-B store.
+            // (c+1 past the last cell reads the mask words behind: never used, as
+            // the last store of the run ends at plane P-1.)
             for (int k = t0; k < total / 4; k += nt) {
                 const int e = 4 * k;
-                int c = e / P, pl = e - c * P;
-                int v[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    v[j] = ((ow[c] >> pl) & 1u) ? ONE : 0;
-                    if (++pl == P) { pl = 0; c++; }
-                }
-                st16(out + e, v[0], v[1], v[2], v[3]);
+                const int c = e / P, pl = e - c * P;
+                const uint64_t win = (uint64_t)ow[c] | ((uint64_t)ow[c + 1] << P);
+                const uint32_t bits = (uint32_t)(win >> pl);
+                st16(out + e, (bits & 1u) ? ONE : 0, (bits & 2u) ? ONE : 0, (bits & 4u) ? ONE : 0, (bits & 8u) ? ONE : 0);
             }
         } else {
             for (int e = t0; e < total; e += nt) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
@@ -374,17 +429,19 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
         int32_t* out = p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH;
         const int total = NV * HW * MRTS_MASK_CH;
         if ((HW & 1) == 0) {   // HW * 78 % 4 == 0: every env's rows start 16-B aligned
+            // elements e .. e+3 are channels ch .. ch+3 of row r = bits ch+1 .. ch+4 of
+            // its 79-bit word (bit 0 = source); e is a multiple of 4 and a row pair
+            // is 156 elements, so ch is even and only ch = 76 runs into row r+1
+            // (channels 76, 77 = bits 77, 78, then bits 1, 2 of the next row, whose
+            // first word is the word after bit 78's).  One paired LDS read per store.
+            static_assert(MRTS_MASK_CH == 78, "mask row layout");
             for (int k = t0; k < total / 4; k += nt) {
                 const int e = 4 * k;
-                int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH;
-                int v4[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int b = ch + 1;
-                    v4[j] = (int)((mw[3 * r + (b >> 5)] >> (b & 31)) & 1u);
-                    if (++ch == MRTS_MASK_CH) { ch = 0; r++; }
-                }
-                st16(out + e, v4[0], v4[1], v4[2], v4[3]);
+                const int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH, b0 = ch + 1, w = 3 * r + (b0 >> 5);
+                const uint32_t lo = mw[w], hi = mw[w + 1];
+                const uint32_t bits = ch == 76 ? (((lo >> 13) & 3u) | (((hi >> 1) & 3u) << 2))
+                                               : (uint32_t)((((uint64_t)hi << 32) | lo) >> (b0 & 31));
+                st16(out + e, (int)(bits & 1u), (int)((bits >> 1) & 1u), (int)((bits >> 2) & 1u), (int)((bits >> 3) & 1u));
             }
         } else {
             for (int e = t0; e < total; e += nt) {
@@ -740,10 +797,10 @@ __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, Stat
         const int32_t* bp = p.botpa + (size_t)(g - p.nsp_games) * 2 * HW;
         pf.bpa0 = p.bot_ai0 ? bp[c] : 0;   // player 0 bots: MicroRTSBotVecEnv only
         pf.bpa1 = bp[HW + c];
-        if (FB && threadIdx.x < 64) {   // 2 * HW >= 128 words: fusion needs HW > 64
+        if (FB && threadIdx.x < 64) {   // words lane, lane + 64 of the game's 2 * HW (clamped: small maps)
             const int4* aa = p.aa + ((size_t)(g - p.nsp_games) * 2 + 1) * HW * 2;
-            pf.aa = aa[threadIdx.x];
-            pf.aa2 = aa[64 + threadIdx.x];
+            pf.aa = aa[min((int)threadIdx.x, 2 * HW - 1)];
+            pf.aa2 = aa[min(64 + (int)threadIdx.x, 2 * HW - 1)];
         }
     }
     if (p.nmaps == 1) pf.wall = p.map_wall[c];   // else the game's map is known only with genv
@@ -787,6 +844,10 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const int g = blockIdx.x;
     if (game_parked(p, g)) return;   // no tick: its outputs stay zero (mrts_park_games)
     if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
+    if (FB && P == 29 && p.early_bot && g >= p.nsp_games && NT > 64) {   // the early bot's tail arrays start zeroed
+        uint32_t* t = reinterpret_cast<uint32_t*>(smem + fb_tail_offset(HW, p.W, NT));
+        for (int i = threadIdx.x; i < (int)(bots::bot_tail_bytes(HW, p.W) / 4); i += NT) t[i] = 0;
+    }
     const Game G = game_of(p, g);
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
     // the source-unit rows of this lane's first cell, fetched in the same round
@@ -986,6 +1047,9 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // Independent ready sets (no attack, no two harvests of one pile) commute:
     // every target cell is distinct (moves / produces hold reservations),
     // resources only add up, and produced units take ids in issue order.
+    // (Attacks on cells no other ready action touches would commute too; run in
+    // parallel that way they measured neutral at 1024 and slower at 8192 envs:
+    // DESIGN.md §5.)
     int serial = 0, nprodr = 0;
     for (int i = threadIdx.x; i < nready; i += NT) {
         L.act[L.list[i]] = 0;   // unitActions.remove
@@ -1081,9 +1145,12 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         // next tick's bot at once while waves 1.. build the output words and
         // stream them, meeting at an LDS counter instead of a workgroup barrier.
         __syncthreads();
+        bot_setup_workgroup<NT>(p, smem, smem + fb_tail_offset(HW, p.W, NT), L.wall, L.ballot);
+        __syncthreads();
         if (threadIdx.x < 64) {
             __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
-            bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT), L.wall);
+            bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT), L.wall,
+                                 true);
         }
         else
             emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, 64, early_cnt);
@@ -1415,7 +1482,13 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
     return hipGetLastError();
 }
 
+// Workgroup size of a map size: one lane per cell up to 256 lanes; the bot-fused
+// step needs a wave besides the bot's, so maps of <= 64 cells take 128 lanes there.
+__host__ __device__ inline int step_nt(int HW, bool fused) { return HW <= 64 && !fused ? 64 : HW <= 128 ? 128 : 256; }
+
 static hipError_t dispatch(const EngineParams& p, int kind, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
+    if (kind == 2 && p.fuse_bots) return step_nt(p.HW, true) == 128 ? launch_all<128>(p, kind, s, games, maps, count)
+                                                                      : launch_all<256>(p, kind, s, games, maps, count);
     if (p.HW <= 64) return launch_all<64>(p, kind, s, games, maps, count);
     if (p.HW <= 128) return launch_all<128>(p, kind, s, games, maps, count);
     return launch_all<256>(p, kind, s, games, maps, count);
@@ -1460,14 +1533,8 @@ hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, in
                        p->W, p->H, size, rgb);
     return hipGetLastError();
 }
-int mrts_engine_early_bot_ok(int HW, int W) {
-    const int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
-    return NT > 64 && mrts::early_bot_disjoint(HW, W, NT) ? 1 : 0;
-}
-size_t mrts_engine_fused_lds_bytes(int HW, int W) {
-    const int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
-    return mrts::fb_lds_bytes(HW, W, NT);
-}
+int mrts_engine_early_bot_ok(int HW, int W) { return mrts::early_bot_disjoint(HW, W, mrts::step_nt(HW, true)) ? 1 : 0; }
+size_t mrts_engine_fused_lds_bytes(int HW, int W) { return mrts::fb_lds_bytes(HW, W, mrts::step_nt(HW, true)); }
 size_t mrts_engine_lds_bytes(int HW, int W) {
     int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
     return mrts::lds_bytes(HW, W, NT);

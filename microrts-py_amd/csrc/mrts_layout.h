@@ -35,7 +35,8 @@
  *   NPA   entries of the bot PlayerAction handed from k_bot to k_step
  * rollout statistics, never reset (mrts_game_stats):
  *   SERIAL   ticks whose ready set executed in order on one lane (attacks, shared piles)
- *   ORDERED  action rows issued on the ordered (one-lane) path
+ *   ORDERED  action rows issued on the ordered (one-lane) path: the agent's and the device bots' rows
+ *            still CAND after the lane-parallel pass (k_step compacts both kinds into one list)
  *   EPISODES auto-resets (gameover or max_steps) */
 enum { MRTS_G_TIME = 0, MRTS_G_RES0, MRTS_G_RES1, MRTS_G_NEXT_UID, MRTS_G_STEPS, MRTS_G_MAP, MRTS_G_ERR, MRTS_G_AA_N,
        MRTS_G_TICKS, MRTS_G_NPA, MRTS_G_AA_N0, MRTS_G_NPA0, MRTS_G_SERIAL, MRTS_G_ORDERED, MRTS_G_EPISODES,

@@ -835,6 +835,14 @@ class MicroRTSSizeCyclingVecEnv:
       obs, rew, done, infos = env.step(acts) # acts: list over env.sizes; rew / done: (N,) over all envs
       env.bucket                             # (N,) index into env.sizes of each env's current map
 
+    Random bots (randomBiasedAI, randomAI) key their Philox stream on (unit, the
+    game's tick counter in the engine it plays in, game).  A parked game's counter
+    does not advance, so after a move to another size the stream continues from
+    that engine's counter for the game, not from the ticks played elsewhere.  No
+    reference fixture holds these streams (the Java bots draw from an unseeded
+    java.util.Random): parity unpinned, and tests/test_gpu_size_cycling.py uses
+    deterministic bots.
+
     Rows of envs that play in another engine are zero in every list entry, so a
     policy can run each size's batch as it is.  Device tensors only (the
     return_tensors=True contract)."""

@@ -133,6 +133,7 @@ class JNIGridnetVecClient:
             self._src = torch.empty((n, hw), dtype=torch.int32, device=self.device)
             self._rew = torch.zeros((n, 6), dtype=torch.float64, device=self.device)
             self._done = torch.zeros((n, 6), dtype=torch.uint8, device=self.device)
+        self._raw_cache = None   # host copy of _raw_obs for the current engine state (_raw_host)
         L = _native.lib()
         _native.check(L.mrts_bind_workspace(self._h, self._ws.data_ptr(), self._stream()), self._h, "bind_workspace")
         self.utt_json = L.mrts_utt_json(self._h).decode()
@@ -145,11 +146,21 @@ class JNIGridnetVecClient:
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    def _raw_host(self):
+        """Every env's raw observation as a host array, computed (k_raw + one D2H) once
+        per engine state: reset, gameStep and per-game resets invalidate it, so the
+        reference's cycling loop (one getResponse per finished env, vec_env.py:1044-1054)
+        costs one kernel per tick, not one per finished env."""
+        if self._raw_cache is None:
+            _native.check(_native.lib().mrts_get_raw_obs(self._h, self._stream(), self._raw_obs.data_ptr()), self._h, "raw_obs")
+            self._raw_cache = self._raw_obs.cpu().numpy()
+        return self._raw_cache
+
     def _response(self):
-        _native.check(_native.lib().mrts_get_raw_obs(self._h, self._stream(), self._raw_obs.data_ptr()), self._h, "raw_obs")
-        return Response(self._raw_obs.cpu().numpy(), self._rew.cpu().numpy(), self._done.cpu().numpy().astype(bool))
+        return Response(self._raw_host().copy(), self._rew.cpu().numpy(), self._done.cpu().numpy().astype(bool))
 
     def reset(self, players):
+        self._raw_cache = None
         _native.check(_native.lib().mrts_reset(self._h, self._stream(), self._obs.data_ptr()), self._h, "reset")
         self._rew.zero_()
         self._done.zero_()
@@ -173,6 +184,7 @@ class JNIGridnetVecClient:
                 src[i, r[:, 0]] = 1
         a = torch.from_numpy(dense).to(self.device)
         s = torch.from_numpy(src).to(self.device)
+        self._raw_cache = None
         _native.check(_native.lib().mrts_step(self._h, self._stream(), a.data_ptr(), s.data_ptr(), self._obs.data_ptr(),
                                               self._rew.data_ptr(), self._done.data_ptr()), self._h, "step")
         return self._response()
@@ -183,6 +195,7 @@ class JNIGridnetVecClient:
         return _native.add_map(self._h, self._stream(), full)
 
     def _reset_game(self, game, map_id):
+        self._raw_cache = None
         g = (ctypes.c_int32 * 1)(game)
         m = (ctypes.c_int32 * 1)(map_id)
         _native.check(_native.lib().mrts_reset_games(self._h, self._stream(), g, m, 1, self._obs.data_ptr()), self._h,
@@ -192,8 +205,7 @@ class JNIGridnetVecClient:
         self._done[envs] = 0
 
     def _env_response(self, env):
-        _native.check(_native.lib().mrts_get_raw_obs(self._h, self._stream(), self._raw_obs.data_ptr()), self._h, "raw_obs")
-        return Response(self._raw_obs[env].cpu().numpy(), self._rew[env].cpu().numpy(),
+        return Response(self._raw_host()[env].copy(), self._rew[env].cpu().numpy(),
                         self._done[env].cpu().numpy().astype(bool))
 
     def _render(self, env, rgb):

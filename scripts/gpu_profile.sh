@@ -30,5 +30,6 @@ done
 cp "$O/pmc_latest.json" profiles/pmc_latest.json
 timeout -k 10 300 python bench.py > "$O/bench.json" 2> "$O/bench.err"
 timeout -k 10 300 python bench.py --workload coac --envs-per-gpu 1024 --no-cpu-baseline > "$O/bench_coac.json" 2> "$O/bench_coac.err"
-cat "$O/bench.json" "$O/bench_coac.json"
+timeout -k 10 300 python bench.py --workload mixed --no-cpu-baseline > "$O/bench_mixed.json" 2> "$O/bench_mixed.err"
+cat "$O/bench.json" "$O/bench_coac.json" "$O/bench_mixed.json"
 echo done > "$O/DONE"

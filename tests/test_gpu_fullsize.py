@@ -134,3 +134,64 @@ def test_fullsize_2000_tick_episode_1024():
     assert (st[:256, 5] >= 1).all()            # every unstaggered game finished an episode
     assert ends >= 512                         # games 0..255 (both views) reset at tick 2000
     assert g.error_flags() == 0
+
+
+@pytest.mark.timeout(1200)
+def test_fullsize_headline_8192_staggered_2000_ticks():
+    """The headline configuration itself (8192 selfplay envs, 16x16 basesWorkers,
+    max_steps 2000) through the bench's own loop for 2100 ticks: the device sampler
+    (mrts_sample_actions_src, Philox) on the GPU and the oracle's identical C sampler
+    (ovec_bench_steps) on the host, every game reset at its staggered pre-roll tick
+    (bench.stagger_plan) -- so over the run every game goes through a whole 2000-tick
+    episode and the window after tick 2000 holds games at every phase, as in the
+    timed bench window.  Raw rewards and dones are compared every tick; the whole
+    obs, mask and source tensors every 50 ticks and at the end."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from gym_microrts import _native
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv
+
+    n, m, seed = 8192, "maps/16x16/basesWorkers16x16.xml", 1
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=n, num_bot_envs=0, max_steps=2000, map_paths=[m], reward_weight=W,
+                               return_tensors=True, obs_dtype=torch.int32)
+    o = OracleVecEnv(n, 0, [os.path.join(MAPS, m)], max_steps=2000, reward_weight=W)
+    dev, hw, lib = g.device, 256, _native.lib()
+    act = torch.empty((n, hw, 7), dtype=torch.int64, device=dev)
+
+    def same(gpu, host, what, s):
+        assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"{what} differs at tick {s}"
+
+    same(g.reset(), o.reset(), "reset obs", -1)
+    plan = bench.stagger_plan(n // 2, 2000)
+    ends = 0
+    for s in range(2100):
+        g.get_action_mask()
+        _native.check(bench.sample(lib, "src", g._mask, g._src, n, hw, 0, seed, s, act), None, "sample")
+        og, _, dg, ig = g.step(act)
+        _, ro, do = o.bench_steps(1, seed, s)
+        same(ig._raw, ro, "raw rewards", s)
+        same(g._done, do.astype(np.uint8), "dones", s)
+        ends += int(do[:, 0].sum())
+        if s < 2000 and plan[s]:
+            g.reset_games(plan[s])
+            for k in plan[s]:
+                o.reset_game(k, 0)
+        if s % 50 == 0 or s == 2099:
+            same(og, o.encode(o.raw_obs()), "obs", s)
+            full = o.get_action_mask_full()
+            same(g.get_action_mask(), full[:, :, 1:], "mask", s)
+            same(g.source_unit_mask, full[:, :, 0], "source", s)
+            del full
+    st = g.game_stats()
+    # games 0..204 restarted at pre-roll ticks <= 99 (floor(g * 2000 / 4096)): each then played a whole
+    # 2000-tick episode to its time limit within the run (or ended earlier by gameover)
+    assert (st[:205, 5] >= 1).all()
+    assert ends >= 2 * 205
+    assert g.error_flags() == 0
+    g.close()
+    o.close()
