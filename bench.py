@@ -385,7 +385,32 @@ def run_gpu(args, rank, world, local_rank):
     kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
     G = nsp // 2 + nbot
     src_rows = int(env._src.sum().item())   # source cells of the last step (sampler bytes)
+    if not args.no_kernel_events and rank == 0:
+        stats["box_write_ceiling"] = write_ceiling(dev, kernel_bytes(G, n, hw, sum(env.num_planes))["step"])
     return elapsed, kern, flags, env.height * env.width, G, env.num_envs, sum(env.num_planes), src_rows, stats
+
+
+def write_ceiling(dev, nbytes, reps=20):
+    """This box's write rate for the step kernel's byte count, measured in the same run:
+    back-to-back torch fill_ of one buffer of that size (HIP events around each fill on
+    the current stream; each fill pays the previous one's dirty lines, as k_step pays the
+    sampler's).  Context for roofline.frac, which is priced against the 8 TB/s peak: box
+    states differ by ~10-15 %."""
+    import torch
+
+    buf = torch.empty(int(nbytes) // 4, dtype=torch.int32, device=dev)
+    buf.fill_(1)
+    t = []
+    for i in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        buf.fill_(i)
+        b.record()
+        t.append((a, b))
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in t)[reps // 2]
+    del buf
+    return {"bytes": int(nbytes), "fill_ms": round(ms, 4), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1)}
 
 
 def _coll_device(dev):
@@ -547,6 +572,9 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": tb,
                     "kernel": "step (all size buckets)", "avg_launch_ms": round(tms, 4)}
+        wc = stats.get("box_write_ceiling")
+        if roof and wc and roof.get("kernel") == "step":
+            roof["frac_of_box_write_ceiling"] = round(roof["achieved"] / wc["GBps"], 4)
         env_step_bytes = hw * (4 * P + 312 + 56 + 32) + 64   # SURVEY.md §8d whole-step formula
         out = {
             "metric": METRIC,

@@ -7,7 +7,7 @@ sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "microrts-py_amd
 import bench
 from gym_microrts import _native
 from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
-n = 8192
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 dev = torch.device("cuda", 0)
 env = MicroRTSGridModeVecEnv(n, 0, max_steps=2000, map_paths=[bench.MAP], reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]),
                              device=dev, return_tensors=True)
@@ -32,7 +32,7 @@ for s in range(s0, s0 + 30):
 a = np.stack(acc) / 100.0   # us (100 MHz)
 start, logic, end = a[:, :, 0], a[:, :, 2], a[:, :, 9]
 span = end.max(1)
-per_game_bytes = 948428800 / G
+per_game_bytes = 948428800 / 4096
 out = {"span_us": float(span.mean()), "game_start_us": {q: float(np.percentile(start, q)) for q in (0, 25, 50, 75, 90, 100)},
        "logic_us (start->stored)": {q: float(np.percentile(logic - start, q)) for q in (10, 50, 90, 99)},
        "stream_us (stored->end)": {q: float(np.percentile(end - logic, q)) for q in (10, 50, 90, 99)},
