@@ -180,7 +180,8 @@ int mrts_add_map(mrts_vec *h, void *stream, const char *path, int32_t *index);
 int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int32_t hw, int32_t env0, uint64_t seed,
                         uint32_t step, int64_t *actions);
 
-/* Same stream and output as mrts_sample_actions, given the source channel too:
+/* Same stream and output as mrts_sample_actions, given the source channel too
+ * (num_envs * hw must stay below 2^31 - 64: MRTS_EINVAL otherwise):
  * mask rows of cells whose source is 0 are all zero (getMasks), so only the
  * rows of source cells are read.  Every row's 7 components are still written. */
 int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t num_envs, int32_t hw,

@@ -57,7 +57,8 @@ struct Lds {
 // L.sc[0 .. MRTS_GENV_WORDS) mirrors genv (load_game / store_game)
 enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_UID = MRTS_G_NEXT_UID,
        SC_STEPS = MRTS_G_STEPS, SC_MAP = MRTS_G_MAP, SC_ERR = MRTS_G_ERR, SC_AA_N = MRTS_G_AA_N, SC_TICKS = MRTS_G_TICKS,
-       SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_RPROD = 29 /* ready produces */, SC_WORDS = 32 };
+       SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_RPROD = 29 /* ready produces */,
+       SC_OVER = 30 /* a pending produce is over its owner's budget */, SC_HAS = 31 /* bit q: player q has a unit */, SC_WORDS = 32 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -558,6 +559,16 @@ __device__ __forceinline__ int unchecked_pos(const Grid& gd, int c, int dir) {  
 
 __device__ __forceinline__ int res_of(const Lds& L, int player) { return L.sc[SC_RES0 + player]; }
 
+// Step (2a)'s target-position claims of a move / produce row: bit b of claim[0..posw)
+// when >= 1 row targets position b (x + y * W + W, unchecked), of claim[posw..) when >= 2.
+__device__ __forceinline__ void claim_target(const Lds& L, const Grid& gd, int c, int code, int posw) {
+    const int ty = code_type(code);
+    if (ty != A_MOVE && ty != A_PRODUCE) return;
+    const int b = unchecked_pos(gd, c, code_param(code)) + gd.W;
+    const uint32_t bit = 1u << (b & 31);
+    if (atomicOr(&L.claim[b >> 5], bit) & bit) atomicOr(&L.claim[posw + (b >> 5)], bit);
+}
+
 // PlayerAction.fromVectorAction consistency filter + GameState.issueSafe/issue
 // for one player's PlayerAction (lane 0 only).  Entries are list[0..n) in
 // PlayerAction order with their codes in L.aux: the agent's rows (ascending
@@ -784,6 +795,7 @@ struct StatePf {
     int bpa0, bpa1;   // bot games: entry `lane` of the bot PlayerActions (player 0 / 1)
     int4 aa, aa2;     // bot-fused games, lanes < 64: words lane, lane + 64 of the bot's abstract actions
     int wall;         // single-map batches: this cell's terrain
+    int map;          // the game's map (genv[MRTS_G_MAP], every lane: no barrier before the terrain load)
 };
 template <int NT, bool FB>
 __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, StatePf& pf) {
@@ -804,19 +816,20 @@ __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, Stat
         }
     }
     if (p.nmaps == 1) pf.wall = p.map_wall[c];   // else the game's map is known only with genv
+    else pf.map = p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
 }
 template <int NT>
 __device__ __forceinline__ void commit_game(const EngineParams& p, const Lds& L, const StatePf& pf) {
     if (threadIdx.x < MRTS_GENV_WORDS) L.sc[threadIdx.x] = pf.genv;
-    __syncthreads();
-    const int HW = p.HW, map = L.sc[SC_MAP];
+    const int HW = p.HW;
     if ((int)threadIdx.x < HW) {
         const int c = threadIdx.x;
         L.unit[c] = (uint32_t)pf.cell.x;
         L.uid[c] = pf.cell.y;
         L.act[c] = (uint32_t)pf.cell.z;
         L.seq[c] = (uint32_t)pf.cell.w;
-        L.wall[c] = p.nmaps == 1 ? (uint8_t)pf.wall : p.map_wall[(size_t)map * HW + c];
+        L.wall[c] = p.nmaps == 1 ? (uint8_t)pf.wall : p.map_wall[(size_t)pf.map * HW + c];
+        L.resv[c] = -1;   // reservation holders (step 1)
     }
     __syncthreads();
 }
@@ -849,7 +862,13 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         for (int i = threadIdx.x; i < (int)(bots::bot_tail_bytes(HW, p.W) / 4); i += NT) t[i] = 0;
     }
     const Game G = game_of(p, g);
+    // Barriers: each phase below is ordered after the last one that wrote what it
+    // reads from OTHER lanes; a phase that reads only its own lane's cells (the
+    // same c = threadIdx.x + k * NT walk) follows its predecessor without one.
+    // Everything zeroed or initialised here is first read after commit_game's barrier.
     if (threadIdx.x < SC_WORDS) L.sc[threadIdx.x] = 0;
+    const int posw = (HW + 2 * p.W) / 32 + 1;   // position words (targets as x + y * W + W)
+    for (int i = threadIdx.x; i < 2 * posw; i += NT) L.claim[i] = 0;
     // the source-unit rows of this lane's first cell, fetched in the same round
     // trip as the game state (the decode below needs both)
     int src_pre[2] = {0, 0};
@@ -859,20 +878,35 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     } else if ((int)threadIdx.x < HW) {
         for (int v = 0; v < G.nviews; v++) src_pre[v] = p.src[(size_t)(G.env0 + v) * HW + threadIdx.x];
     }
-    __syncthreads();
-    if (pf_ok) commit_game<NT>(p, L, pf);
-    else load_game<NT>(p, L, g);
+    if (pf_ok) {
+        commit_game<NT>(p, L, pf);
+    } else {
+        for (int c = threadIdx.x; c < HW; c += NT) L.resv[c] = -1;
+        load_game<NT>(p, L, g);
+    }
     const int time = L.sc[SC_TIME];
+    const int steps0 = L.sc[SC_STEPS], map_now = L.sc[SC_MAP];   // read before any lane can rewrite them (auto-reset)
     // bot-vs-bot game (MicroRTSBotVecEnv): player 0's PlayerAction comes from k_bot too
     const bool bot0 = !G.selfplay && p.bot_ai0 && p.bot_ai0[g - p.nsp_games] >= 0;
 
     // (1) decode the rows of every idle unit whose cell is in source_unit_mask
     //     (vec_env.py:972-974) + Unit.canExecuteAction, lane-parallel.
+    // + pending move/produce reservations (ResourceUsage of unitActions) and whether
+    //   a pending produce is over its owner's budget; + the target positions the
+    //   agent's move / produce rows claim (step 2a)
     for (int c = threadIdx.x; c < HW; c += NT) {
         uint32_t u = L.unit[c], nw = 0;
         int ow = u_owner(u);
-        L.resv[c] = -1;
-        if (u != 0 && ow >= 0 && L.act[c] == 0) {
+        const uint32_t pa = L.act[c];
+        if (pa) {
+            const int code = act_code(pa), ty = code_type(code);
+            if (ty == A_MOVE || ty == A_PRODUCE) {
+                const int n = nb_cell(gd, c, code_param(code));
+                if (n >= 0) L.resv[n] = c;
+                if (ty == A_PRODUCE && ut_cost(code_utype(code)) > res_of(L, u_owner(u))) L.sc[SC_OVER] = 1;
+            }
+        }
+        if (u != 0 && ow >= 0 && pa == 0) {
             int view = G.selfplay ? ow : (ow == 0 && !bot0 ? 0 : -1);
             if (view >= 0) {
                 const size_t row = (size_t)(G.env0 + view) * HW + c;
@@ -897,17 +931,18 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
                     if (code >= 0) {
                         bool lg = legal_code(gd, c, code, L.unit, L.wall, res_of(L, ow));
                         nw = CAND | (lg ? LEGAL : 0u) | (uint32_t)code;
+                        claim_target(L, gd, c, code, posw);
                     }
                 }
             }
         }
         L.aux[c] = nw;
     }
-    __syncthreads();
     // the device bot's PlayerAction for player 1 (k_bot, computed on the state
     // before this tick's issues: JNIGridnetClient.gameStep order)
     const int npa = (!G.selfplay && p.botpa) ? L.sc[SC_NPA] : 0;
     const int npa0 = bot0 ? L.sc[MRTS_G_NPA0] : 0;
+    if (npa | npa0) __syncthreads();   // the bot rows' aux words after the decode's (which zeroed them)
     // entry k of player q's PlayerAction: lane k's prefetched word (maps with HW <= NT),
     // else a load; its position in the PlayerAction (the LinkedHashMap rank) rides in aux
     for (int q = 0; q < 2; q++) {
@@ -919,20 +954,11 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             (q ? L.blist : L.blist0)[k] = c;
             L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, q)) ? LEGAL : 0u) | ((uint32_t)k << 12) |
                        (uint32_t)code;
+            claim_target(L, gd, c, code, posw);
         }
     }
-    __syncthreads();
-    // pending move/produce reservations (ResourceUsage of unitActions)
-    for (int c = threadIdx.x; c < HW; c += NT) {
-        uint32_t a = L.act[c];
-        if (a) {
-            int code = act_code(a), ty = code_type(code);
-            if (ty == A_MOVE || ty == A_PRODUCE) {
-                int n = nb_cell(gd, c, code_param(code));
-                if (n >= 0) L.resv[n] = c;
-            }
-        }
-    }
+    // (the compaction's barriers order the reservations, claims, SC_OVER and the
+    // bot rows before everything below)
     int nprod = compact_cells<NT>(HW, [&](int c) {
         uint32_t a = L.act[c];
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
@@ -947,25 +973,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     //      its LinkedHashMap rank is still its cell (agent rows) or its position in
     //      the bot's PlayerAction.  Everything else takes the ordered path (2b).
     {
-        const int posw = (HW + 2 * p.W) / 32 + 1;
-        for (int i = threadIdx.x; i < 2 * posw; i += NT) L.claim[i] = 0;
-        int over = 0;
-        for (int k = threadIdx.x; k < nprod; k += NT) {
-            const int pc = L.prod[k];
-            over |= ut_cost(code_utype(act_code(L.act[pc]))) > res_of(L, u_owner(L.unit[pc]));
-        }
-        over = __syncthreads_or(over);
-        for (int c = threadIdx.x; c < HW; c += NT) {
-            const uint32_t nw = L.aux[c];
-            if (!(nw & CAND)) continue;
-            const int code = (int)(nw & 0xFFFu), ty = code_type(code);
-            if (ty != A_MOVE && ty != A_PRODUCE) continue;
-            const int b = unchecked_pos(gd, c, code_param(code)) + p.W;
-            const uint32_t bit = 1u << (b & 31);
-            if (atomicOr(&L.claim[b >> 5], bit) & bit) atomicOr(&L.claim[posw + (b >> 5)], bit);
-        }
-        __syncthreads();
-        if (!over) {
+        if (!L.sc[SC_OVER]) {
             for (int c = threadIdx.x; c < HW; c += NT) {
                 const uint32_t nw = L.aux[c];
                 if (!(nw & CAND)) continue;
@@ -993,7 +1001,8 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
                 if (ct == A_ATTACK) atomicAdd(&L.sc[SC_R0 + 6 * q + 4], 1);
                 L.aux[c] = nw & ~CAND;   // issued
             }
-            __syncthreads();
+            // no barrier: the compaction below reads each cell's aux word on the
+            // lane that wrote it, and its barriers order the rest before step (2b)
         }
     }
     // (2b) the ordered path for the rest
@@ -1007,7 +1016,8 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         else if (npa > 0) issue_player(p, L, gd, 1, L.blist, npa, false);
     }
     __syncthreads();
-    // (3) fillWithNones(gs, player, 1) for every idle unit (both players)
+    // (3) fillWithNones(gs, player, 1) for every idle unit (both players); the
+    //     cycle's first passes below read each cell on the lane that wrote it
     for (int c = threadIdx.x; c < HW; c += NT) {
         uint32_t u = L.unit[c];
         if (u != 0 && u_owner(u) >= 0 && L.act[c] == 0) {
@@ -1015,7 +1025,6 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             L.seq[c] = seq_make(time, u_owner(u), 4095);
         }
     }
-    __syncthreads();
     // (4) GameState.cycle(): time++, execute ready assignments in issue order
     const int now = time + 1;
     for (int c = threadIdx.x; c < HW; c += NT) {
@@ -1029,7 +1038,6 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     }, L.list, L.ballot, [&](int pos, int c) { L.aux[pos] = L.seq[c]; });
     // snapshots of the ready assignments in LinkedHashMap (issue-sequence)
     // order: lane-parallel rank by sequence word (unique among non-NONE actions)
-    const int posw = (HW + 2 * p.W) / 32 + 1;
     for (int i = threadIdx.x; i < posw; i += NT) L.claim[i] = 0;
     if (threadIdx.x == 0) L.sc[SC_RPROD] = 0;
     for (int i = threadIdx.x; i < nready; i += NT) {
@@ -1079,6 +1087,17 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         }
     }
     __syncthreads();
+    // (5) PhysicalGameState.gameover / winner: which players still have units,
+    //     ORed into SC_HAS behind the barrier the scalar updates need anyway
+    {
+        int hb = 0;
+        for (int c = threadIdx.x; c < HW; c += NT) {
+            const uint32_t u = L.unit[c];
+            const int ow = u_owner(u);
+            if (u != 0 && (ow == 0 || ow == 1)) hb |= 1 << ow;
+        }
+        if (hb) atomicOr(&L.sc[SC_HAS], hb);
+    }
     if (threadIdx.x == 0) {
         L.sc[SC_TIME] = now;
         L.sc[SC_TICKS]++;
@@ -1089,19 +1108,12 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             L.sc[SC_UID] += L.sc[SC_RPROD];
     }
     __syncthreads();
-    // (5) PhysicalGameState.gameover / winner
-    int has0 = 0, has1 = 0;
-    for (int c = threadIdx.x; c < HW; c += NT) {
-        int ow = u_owner(L.unit[c]);
-        has0 |= (L.unit[c] != 0 && ow == 0);
-        has1 |= (L.unit[c] != 0 && ow == 1);
-    }
-    has0 = __syncthreads_or(has0);
-    has1 = __syncthreads_or(has1);
+    const int has = L.sc[SC_HAS];
+    const bool has0 = has & 1, has1 = has & 2;
     const bool gameover = !(has0 && has1);
     const int winner = (has0 && !has1) ? 0 : (has1 && !has0) ? 1 : -1;
     // (6) rewards / done (JNIGridnetVecClient.gameStep terminal handling)
-    const int steps = L.sc[SC_STEPS] + 1;
+    const int steps = steps0 + 1;
     const bool reset = gameover || steps >= p.max_steps;
     if (threadIdx.x < 6 * G.nviews) {
         int v = threadIdx.x / 6, k = threadIdx.x % 6;
@@ -1120,14 +1132,14 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         p.reward[env] = s;
         p.done0[env] = (uint8_t)(reset ? 1 : 0);
     }
-    __syncthreads();
+    // (no barrier: the rewards read only SC_R0.. words, which the reset leaves
+    // alone, and nothing above reads the cell arrays it rewrites)
     if (reset) {
-        reset_into_lds<NT>(p, L, L.sc[SC_MAP]);
+        reset_into_lds<NT>(p, L, map_now);
         if (threadIdx.x == 0) {
             L.sc[SC_AA_N] = L.sc[MRTS_G_AA_N0] = 0;   // ai1 / ai2.reset()
             L.sc[MRTS_G_EPISODES]++;
         }
-        __syncthreads();
     } else if (threadIdx.x == 0) {
         L.sc[SC_STEPS] = steps;
     }
@@ -1242,14 +1254,17 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
 // per component k, a uniform pick among the valid entries (uniform over all
 // entries when none is valid), from two Philox4x32-10 blocks of counter
 // (c, e, step, 0|1) -- the oracle's ovec_sample_actions stream.
-__device__ __forceinline__ void sample_row(uint64_t lo, uint64_t hi, int e, int c, uint64_t seed, uint32_t step, int64_t* out) {
-    uint32_t r[8];
+// The row's eight random words: they depend on (cell, env, step, seed) only, so a
+// caller can draw them while the row's mask bits are still in flight.
+__device__ __forceinline__ void philox_row(int e, int c, uint64_t seed, uint32_t step, uint32_t r[8]) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         uint32_t ctr[4] = {(uint32_t)c, (uint32_t)e, step, (uint32_t)h};
         philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
         r[4 * h] = ctr[0]; r[4 * h + 1] = ctr[1]; r[4 * h + 2] = ctr[2]; r[4 * h + 3] = ctr[3];
     }
+}
+__device__ __forceinline__ void select_row(uint64_t lo, uint64_t hi, const uint32_t r[8], int64_t* out) {
     const int off[7] = {0, 6, 10, 14, 18, 22, 29};
     const int len[7] = {6, 4, 4, 4, 4, 7, 49};
 #pragma unroll
@@ -1267,6 +1282,11 @@ __device__ __forceinline__ void sample_row(uint64_t lo, uint64_t hi, int e, int 
         }
         out[k] = pick;
     }
+}
+__device__ __forceinline__ void sample_row(uint64_t lo, uint64_t hi, int e, int c, uint64_t seed, uint32_t step, int64_t* out) {
+    uint32_t r[8];
+    philox_row(e, c, seed, step, r);
+    select_row(lo, hi, r, out);
 }
 
 // Persistent, software-pipelined: every WAVE owns groups of SW = 32 consecutive
@@ -1394,7 +1414,17 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
     if (row0 >= rows) return;
     const int rb = (int)min(64ll, rows - row0);
     const bool in = lane < rb;
-    const int s = in ? src[row0 + lane] : 0;
+    // unconditional load (tail lanes re-read the last row): no branch around it, so
+    // its wait falls after the row's Philox words, which are drawn while the source
+    // word (and then the mask rows) are in flight
+    const int s_raw = src[row0 + min(lane, rb - 1)];
+    uint32_t r8[8];
+    const unsigned idx = (unsigned)(row0 + lane);   // rows = n * hw < 2^31 (mrts_sample_actions_src checks)
+    const int e = (int)(idx / (unsigned)hw), c = (int)(idx - (unsigned)e * (unsigned)hw);
+    philox_row(env0 + e, c, seed, step, r8);
+#pragma unroll
+    for (int k = 0; k < 8; k++) asm volatile("" : "+v"(r8[k]));   // computed here, not sunk to their use after the loads
+    const int s = in ? s_raw : 0;
     uint64_t pending = __ballot(s != 0);
     uint64_t lo = 0, hi = 0;   // this lane's row as 78 bits
     while (pending) {          // wave-uniform
@@ -1418,11 +1448,7 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
             if (lane == r[k]) { lo = b0; hi = b1; }
         }
     }
-    if (in) {
-        const long long idx = row0 + lane;
-        const int e = (int)(idx / hw), c = (int)(idx - (long long)e * hw);
-        sample_row(lo, hi, env0 + e, c, seed, step, s_out[w] + lane * 7);
-    }
+    if (in) select_row(lo, hi, r8, s_out[w] + lane * 7);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int64_t* ob = act + row0 * 7;   // 16-B aligned: 64 * 56 B per wave
     const int onel = rb * 7, onv = onel >> 1;
