@@ -769,12 +769,9 @@ __device__ __forceinline__ int count_units(const BS& S, const BL& L, int type, b
 
 // WorkerRush / LightRush / HeavyRush / RangedRush (+ PO*)
 __device__ __forceinline__ void behaviours_parallel(BS& S, const BL& L, int army, bool po, bool coac);
-__device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bool po) {
-    if (S.n <= BT && S.naa <= BT) {
-        behaviours_parallel(S, L, army, po, false);
-        translate_actions(S, L);
-        return;
-    }
+// The rush family's behaviours unit by unit (more units or abstract actions than a
+// wave has lanes; behaviours_parallel otherwise).  bot_game translates afterwards.
+__device__ __forceinline__ void rush_serial(BS& S, const BL& L, int army, bool po) {
     const int p = S.player, res = p ? S.res[1] : S.res[0];
     const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
               nbarracks = count_units(S, L, BARRACKS, true);
@@ -805,19 +802,14 @@ __device__ __forceinline__ void rush_get_action(BS& S, const BL& L, int army, bo
             for (int k = head; k < nf; k++) harvest_behavior(S, L, worker(k));
         }
     }
-    translate_actions(S, L);
 }
 
 
 // coacAI: CoacAI's published strategy, restated (oracle/mrts_oracle_ai.c
 // coac_get_action; its free choices are fixed by league.db's outcomes)
 constexpr int COAC_HARVESTERS_PER_BASE = 2, COAC_EXTRA_WORKERS = 2, COAC_BARRACKS_MIN_WORKERS = 2, COAC_DEFENSE_RADIUS = 8;
-__device__ __forceinline__ void coac_get_action(BS& S, const BL& L) {
-    if (S.n <= BT && S.naa <= BT) {
-        behaviours_parallel(S, L, 0, false, true);
-        translate_actions(S, L);
-        return;
-    }
+// (unit by unit, as rush_serial)
+__device__ __forceinline__ void coac_serial(BS& S, const BL& L) {
     const int p = S.player, res = p ? S.res[1] : S.res[0];
     const int nworkers = count_units(S, L, WORKER, true), nbases = count_units(S, L, BASE, true),
               nbarracks = count_units(S, L, BARRACKS, true);
@@ -858,7 +850,6 @@ __device__ __forceinline__ void coac_get_action(BS& S, const BL& L) {
             else harvest_behavior(S, L, w);
         }
     }
-    translate_actions(S, L);
 }
 
 // ---- lane-parallel behaviours (the rush family and coacAI, <= 64 units) --------
@@ -1412,17 +1403,32 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         L.pa[k] = key == 0xFFFFFFFFu ? -1 : (int)(key & 0xFFFFu);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // getAction: the rush family and coacAI decide their abstract actions (lane-
+    // parallel while the unit list and the action list fit a wave, else unit by unit)
+    // and translate them; one call site per routine, with the AI's parameters as
+    // values -- per-AI constant copies made the inlined bot several times larger
+    // (an instruction-cache cost for the latency-bound bot wave)
+    const bool coac = S.ai == MRTS_AI_COAC;
+    int army = -1;
+    bool po = false;
     switch (S.ai) {
-    case MRTS_AI_WORKER_RUSH: rush_get_action(S, L, WORKER, false); break;
-    case MRTS_AI_LIGHT_RUSH: rush_get_action(S, L, LIGHT, false); break;
-    case MRTS_AI_PO_WORKER_RUSH: rush_get_action(S, L, WORKER, true); break;
-    case MRTS_AI_PO_LIGHT_RUSH: rush_get_action(S, L, LIGHT, true); break;
-    case MRTS_AI_PO_HEAVY_RUSH: rush_get_action(S, L, HEAVY, true); break;
-    case MRTS_AI_PO_RANGED_RUSH: rush_get_action(S, L, RANGED, true); break;
-    case MRTS_AI_COAC: coac_get_action(S, L); break;
-    case MRTS_AI_RANDOM_BIASED: random_biased_get_action(S, L); break;
-    case MRTS_AI_RANDOM: random_single_get_action(S, L); break;
+    case MRTS_AI_WORKER_RUSH: army = WORKER; break;
+    case MRTS_AI_LIGHT_RUSH: army = LIGHT; break;
+    case MRTS_AI_PO_WORKER_RUSH: army = WORKER; po = true; break;
+    case MRTS_AI_PO_LIGHT_RUSH: army = LIGHT; po = true; break;
+    case MRTS_AI_PO_HEAVY_RUSH: army = HEAVY; po = true; break;
+    case MRTS_AI_PO_RANGED_RUSH: army = RANGED; po = true; break;
     default: break;
+    }
+    if (coac || army >= 0) {
+        if (S.n <= BT && S.naa <= BT) behaviours_parallel(S, L, coac ? 0 : army, po, coac);
+        else if (coac) coac_serial(S, L);
+        else rush_serial(S, L, army, po);
+        translate_actions(S, L);
+    } else if (S.ai == MRTS_AI_RANDOM_BIASED) {
+        random_biased_get_action(S, L);
+    } else if (S.ai == MRTS_AI_RANDOM) {
+        random_single_get_action(S, L);
     }
     bot_sync<FUSED>();
     for (int i = lane; i < S.npa; i += BT) pa_g[i] = L.pa[i];

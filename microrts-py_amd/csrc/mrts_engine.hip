@@ -58,7 +58,8 @@ struct Lds {
 enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_UID = MRTS_G_NEXT_UID,
        SC_STEPS = MRTS_G_STEPS, SC_MAP = MRTS_G_MAP, SC_ERR = MRTS_G_ERR, SC_AA_N = MRTS_G_AA_N, SC_TICKS = MRTS_G_TICKS,
        SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_RPROD = 29 /* ready produces */,
-       SC_OVER = 30 /* a pending produce is over its owner's budget */, SC_HAS = 31 /* bit q: player q has a unit */, SC_WORDS = 32 };
+       SC_OVER = 30 /* a pending produce is over its owner's budget */,
+       SC_HAS = 31 /* units of player 0 (bits 0..15) and player 1 (16..31) */, SC_WORDS = 32 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -165,11 +166,13 @@ __host__ __device__ inline bool early_bot_disjoint(int HW, int W, int NT) {
 }
 
 // Ordered block-wide compaction: list <- cells c (ascending) with pred(c);
-// put(position, c) is called for every entry as it is written.
+// put(position, c) is called for every entry as it is written.  TAIL = false
+// drops the trailing barrier: the caller orders the list before its readers, and
+// the next compaction must use another s_mask.
 struct NoPut {
     __device__ void operator()(int, int) const {}
 };
-template <int NT, typename F, typename G = NoPut>
+template <int NT, bool TAIL = true, typename F, typename G = NoPut>
 __device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsigned long long* s_mask, G put = G()) {
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -197,7 +200,7 @@ __device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsi
             put(pos, c);
         }
     }
-    __syncthreads();
+    if (TAIL) __syncthreads();
     return total;
 }
 
@@ -414,13 +417,17 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             // elements e .. e+3 are planes pl .. pl+3 of cell c, running on into cell
             // c+1 past plane P-1: one paired LDS read (cells c, c+1) per 16-B store.
             // (c+1 past the last cell reads the mask words behind: never used, as
-            // the last store of the run ends at plane P-1.)
+            // the last store of the run ends at plane P-1.)  A one-hot word has no
+            // bit at or above P, so (w0 >> pl) | (w1 << (P - pl)) are the window's
+            // bits.  (c, pl) advance by a constant per trip: no division in the loop.
+            const int dq = 4 * nt / P, dr = 4 * nt - dq * P;
+            int c = 4 * t0 / P, pl = 4 * t0 - c * P;
             for (int k = t0; k < total / 4; k += nt) {
-                const int e = 4 * k;
-                const int c = e / P, pl = e - c * P;
-                const uint64_t win = (uint64_t)ow[c] | ((uint64_t)ow[c + 1] << P);
-                const uint32_t bits = (uint32_t)(win >> pl);
-                st16(out + e, (bits & 1u) ? ONE : 0, (bits & 2u) ? ONE : 0, (bits & 4u) ? ONE : 0, (bits & 8u) ? ONE : 0);
+                const uint32_t bits = (ow[c] >> pl) | (ow[c + 1] << (P - pl));
+                st16(out + 4 * k, (bits & 1u) ? ONE : 0, (bits & 2u) ? ONE : 0, (bits & 4u) ? ONE : 0, (bits & 8u) ? ONE : 0);
+                c += dq;
+                pl += dr;
+                if (pl >= P) { pl -= P; c++; }
             }
         } else {
             for (int e = t0; e < total; e += nt) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
@@ -435,14 +442,21 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             // is 156 elements, so ch is even and only ch = 76 runs into row r+1
             // (channels 76, 77 = bits 77, 78, then bits 1, 2 of the next row, whose
             // first word is the word after bit 78's).  One paired LDS read per store.
+            // (r, ch) advance by a constant per trip; the ch == 76 fix-up is a select,
+            // not a branch.
             static_assert(MRTS_MASK_CH == 78, "mask row layout");
+            const int dq = 4 * nt / MRTS_MASK_CH, dr = 4 * nt - dq * MRTS_MASK_CH;
+            int r = 4 * t0 / MRTS_MASK_CH, ch = 4 * t0 - r * MRTS_MASK_CH;
+            int r3 = 3 * r;   // the row's first word
             for (int k = t0; k < total / 4; k += nt) {
-                const int e = 4 * k;
-                const int r = e / MRTS_MASK_CH, ch = e - r * MRTS_MASK_CH, b0 = ch + 1, w = 3 * r + (b0 >> 5);
+                const int b0 = ch + 1, w = r3 + (b0 >> 5);
                 const uint32_t lo = mw[w], hi = mw[w + 1];
-                const uint32_t bits = ch == 76 ? (((lo >> 13) & 3u) | (((hi >> 1) & 3u) << 2))
-                                               : (uint32_t)((((uint64_t)hi << 32) | lo) >> (b0 & 31));
-                st16(out + e, (int)(bits & 1u), (int)((bits >> 1) & 1u), (int)((bits >> 2) & 1u), (int)((bits >> 3) & 1u));
+                const uint32_t fun = (uint32_t)((((uint64_t)hi << 32) | lo) >> (b0 & 31));
+                const uint32_t bits = ch == 76 ? ((fun & 3u) | ((hi << 1) & 0xCu)) : fun;
+                st16(out + 4 * k, (int)(bits & 1u), (int)((bits >> 1) & 1u), (int)((bits >> 2) & 1u), (int)((bits >> 3) & 1u));
+                r3 += 3 * dq;
+                ch += dr;
+                if (ch >= MRTS_MASK_CH) { ch -= MRTS_MASK_CH; r3 += 3; }
             }
         } else {
             for (int e = t0; e < total; e += nt) {
@@ -730,6 +744,11 @@ __device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s
         if (o == 0) break;
         int hp = u_hp(o) - ut_damage(t);   // VERSION_ORIGINAL: min == max damage
         if (hp <= 0) {                     // GameState.removeUnit (+ its assignment)
+            const int vo = u_owner(o);
+            if (vo == 0 || vo == 1) {      // the players' unit counts (k_step's SC_HAS)
+                if (PAR) atomicSub(&L.sc[SC_HAS], vo ? 1 << 16 : 1);
+                else L.sc[SC_HAS] -= vo ? 1 << 16 : 1;
+            }
             L.unit[n] = 0;
             L.uid[n] = 0;
             L.act[n] = 0;
@@ -776,6 +795,10 @@ __device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s
         }
         L.unit[n] = u_make(put, owner, ut_hp(put), 0);
         L.uid[n] = PAR ? produced_uid : L.sc[SC_UID]++;
+        if (owner == 0 || owner == 1) {
+            if (PAR) atomicAdd(&L.sc[SC_HAS], owner ? 1 << 16 : 1);
+            else L.sc[SC_HAS] += owner ? 1 << 16 : 1;
+        }
         L.act[n] = 0;
         L.seq[n] = 0;
         if (PAR) atomicSub(&L.sc[SC_RES0 + owner], ut_cost(put));
@@ -894,9 +917,11 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // + pending move/produce reservations (ResourceUsage of unitActions) and whether
     //   a pending produce is over its owner's budget; + the target positions the
     //   agent's move / produce rows claim (step 2a)
+    int units = 0;   // player 0's units + player 1's << 16 (SC_HAS)
     for (int c = threadIdx.x; c < HW; c += NT) {
         uint32_t u = L.unit[c], nw = 0;
         int ow = u_owner(u);
+        if (u != 0 && (ow == 0 || ow == 1)) units += ow ? 1 << 16 : 1;
         const uint32_t pa = L.act[c];
         if (pa) {
             const int code = act_code(pa), ty = code_type(code);
@@ -938,6 +963,7 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         }
         L.aux[c] = nw;
     }
+    if (units) atomicAdd(&L.sc[SC_HAS], units);
     // the device bot's PlayerAction for player 1 (k_bot, computed on the state
     // before this tick's issues: JNIGridnetClient.gameStep order)
     const int npa = (!G.selfplay && p.botpa) ? L.sc[SC_NPA] : 0;
@@ -957,12 +983,15 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             claim_target(L, gd, c, code, posw);
         }
     }
-    // (the compaction's barriers order the reservations, claims, SC_OVER and the
-    // bot rows before everything below)
-    int nprod = compact_cells<NT>(HW, [&](int c) {
+    // (the compaction's barrier orders the reservations, claims, SC_OVER and the
+    // bot rows before everything below; L.prod is first read by issue_player, behind
+    // the next compaction's barriers, so this one needs no trailing barrier and takes
+    // its ballot words from L.vis, free until phase A: HW / 4 + 8 >= the ceil(HW / NT)
+    // * NT / 8 bytes a compaction needs for every NT <= HW + 64)
+    int nprod = compact_cells<NT, false>(HW, [&](int c) {
         uint32_t a = L.act[c];
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
-    }, L.prod, L.ballot);
+    }, L.prod, reinterpret_cast<unsigned long long*>(L.vis));
     // (2a) rows that interact with nothing else this tick issue lane-parallel: a
     //      row (agent or device bot) that is not a produce and, if a move, whose
     //      target position no other row (either player) and no pending assignment
@@ -1017,7 +1046,10 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     }
     __syncthreads();
     // (3) fillWithNones(gs, player, 1) for every idle unit (both players); the
-    //     cycle's first passes below read each cell on the lane that wrote it
+    //     cycle's first passes below read each cell on the lane that wrote it.
+    //     claim[0, posw) (dead since the decode's claims) is cleared for the ready
+    //     set's harvest-pile check.
+    for (int i = threadIdx.x; i < posw; i += NT) L.claim[i] = 0;
     for (int c = threadIdx.x; c < HW; c += NT) {
         uint32_t u = L.unit[c];
         if (u != 0 && u_owner(u) >= 0 && L.act[c] == 0) {
@@ -1037,9 +1069,14 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
         return a != 0 && act_done(a) <= now;
     }, L.list, L.ballot, [&](int pos, int c) { L.aux[pos] = L.seq[c]; });
     // snapshots of the ready assignments in LinkedHashMap (issue-sequence)
-    // order: lane-parallel rank by sequence word (unique among non-NONE actions)
-    for (int i = threadIdx.x; i < posw; i += NT) L.claim[i] = 0;
-    if (threadIdx.x == 0) L.sc[SC_RPROD] = 0;
+    // order: lane-parallel rank by sequence word (unique among non-NONE actions);
+    // in the same pass, unitActions.remove and whether the set commutes:
+    // independent ready sets (no attack, no two harvests of one pile) do -- every
+    // target cell is distinct (moves / produces hold reservations), resources only
+    // add up, and produced units take ids in issue order.  (Attacks on cells no
+    // other ready action touches would commute too; run in parallel that way they
+    // measured neutral at 1024 and slower at 8192 envs: DESIGN.md §5.)
+    int serial = 0, nprodr = 0;
     for (int i = threadIdx.x; i < nready; i += NT) {
         const int c = L.list[i];
         const uint32_t sq = L.aux[i];
@@ -1049,28 +1086,18 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             rank += (v.x < sq) + (v.y < sq) + (v.z < sq) + (v.w < sq);
         }
         for (; j < nready; j++) rank += L.aux[j] < sq;
-        L.snap[rank] = make_int4(c, (int)L.unit[c], act_code(L.act[c]), L.uid[c]);
-    }
-    __syncthreads();
-    // Independent ready sets (no attack, no two harvests of one pile) commute:
-    // every target cell is distinct (moves / produces hold reservations),
-    // resources only add up, and produced units take ids in issue order.
-    // (Attacks on cells no other ready action touches would commute too; run in
-    // parallel that way they measured neutral at 1024 and slower at 8192 envs:
-    // DESIGN.md §5.)
-    int serial = 0, nprodr = 0;
-    for (int i = threadIdx.x; i < nready; i += NT) {
-        L.act[L.list[i]] = 0;   // unitActions.remove
-        const int4 sn = L.snap[i];
-        const int ty = code_type(sn.z);
+        const int code = act_code(L.act[c]), ty = code_type(code);
+        L.snap[rank] = make_int4(c, (int)L.unit[c], code, L.uid[c]);
+        L.act[c] = 0;   // unitActions.remove (each ready cell is read by its own lane only)
         if (ty == A_ATTACK) serial = 1;
         nprodr += ty == A_PRODUCE;
         if (ty == A_HARVEST) {
-            const int n = nb_cell(gd, sn.x, code_param(sn.z));
+            const int n = nb_cell(gd, c, code_param(code));
             if (n >= 0 && (atomicOr(&L.claim[n >> 5], 1u << (n & 31)) >> (n & 31)) & 1u) serial = 1;
         }
     }
-    if (nprodr) atomicAdd(&L.sc[SC_RPROD], nprodr);   // the ids the produced units take
+    if (nprodr) atomicAdd(&L.sc[SC_RPROD], nprodr);   // the ids the produced units take (SC_RPROD starts at 0)
+    const int uid0 = L.sc[SC_UID];   // read before lane 0 may advance it (below)
     serial = __syncthreads_or(serial);
     if (serial) {
         if (threadIdx.x == 0)
@@ -1080,36 +1107,28 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
             const int4 sn = L.snap[i];
             int puid = -1;
             if (code_type(sn.z) == A_PRODUCE) {
-                puid = L.sc[SC_UID];
+                puid = uid0;
                 for (int j = 0; j < i; j++) puid += code_type(L.snap[j].z) == A_PRODUCE;
             }
             execute_one<true>(L, gd, sn, puid);
         }
     }
-    __syncthreads();
-    // (5) PhysicalGameState.gameover / winner: which players still have units,
-    //     ORed into SC_HAS behind the barrier the scalar updates need anyway
-    {
-        int hb = 0;
-        for (int c = threadIdx.x; c < HW; c += NT) {
-            const uint32_t u = L.unit[c];
-            const int ow = u_owner(u);
-            if (u != 0 && (ow == 0 || ow == 1)) hb |= 1 << ow;
-        }
-        if (hb) atomicOr(&L.sc[SC_HAS], hb);
-    }
+    // (no barrier: the scalars below are lane 0's, SC_UID is no longer read, and the
+    // unit counts -- kept by execute_one -- are read behind the next barrier)
     if (threadIdx.x == 0) {
         L.sc[SC_TIME] = now;
         L.sc[SC_TICKS]++;
         L.sc[MRTS_G_SERIAL] += serial;      // rollout statistics (mrts_game_stats)
         L.sc[MRTS_G_ORDERED] += nrows;
-        if (now >= MRTS_MAX_TIME) L.sc[SC_ERR] |= MRTS_ERR_TIME_OVERFLOW;
+        if (now >= MRTS_MAX_TIME) atomicOr(&L.sc[SC_ERR], MRTS_ERR_TIME_OVERFLOW);   // the executing lanes may be ORing too
         if (!serial)
             L.sc[SC_UID] += L.sc[SC_RPROD];
     }
     __syncthreads();
+    // (5) PhysicalGameState.gameover / winner: the unit counts of the decode pass,
+    //     less the units attacks removed, plus the produced ones (execute_one)
     const int has = L.sc[SC_HAS];
-    const bool has0 = has & 1, has1 = has & 2;
+    const bool has0 = (has & 0xFFFF) != 0, has1 = (has >> 16) != 0;
     const bool gameover = !(has0 && has1);
     const int winner = (has0 && !has1) ? 0 : (has1 && !has0) ? 1 : -1;
     // (6) rewards / done (JNIGridnetVecClient.gameStep terminal handling)
@@ -1149,28 +1168,28 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     // + getMasks of the next tick (bound mask outputs): every read of this
     //   game's source rows (phase 1) is behind the barriers above
     const bool botg = FB && g >= p.nsp_games && NT > 64;
-    if (FB && P == 29 && botg && p.early_bot) {
-        // Early bot (full observability: the bot writes none of the arrays phase A
-        // reads -- unit / act / wall stay as stored, the step's scalars and
-        // visibility words are left alone, its small arrays go to the tail region):
-        // once store_game has read the arrays the bot reuses, wave 0 starts the
-        // next tick's bot at once while waves 1.. build the output words and
-        // stream them, meeting at an LDS counter instead of a workgroup barrier.
+    // Early bot (P == 29, p.early_bot: full observability, and for this size the bot
+    // writes none of the arrays phase A reads -- unit / act / wall stay as stored, the
+    // step's scalars and visibility words are left alone, its small arrays go to the
+    // tail region): once store_game has read the arrays the bot reuses, the workgroup
+    // builds the bot's setup, then wave 0 starts the next tick's bot at once while
+    // waves 1.. build the output words and stream them, meeting at an LDS counter
+    // instead of a workgroup barrier.  Otherwise wave 0 helps with phase A and starts
+    // the bot behind its barrier (the step's arrays are dead by then: only L.outw is
+    // read on).  One bot_game call site for both: the inlined bot is most of this
+    // kernel's code.
+    const bool early = FB && P == 29 && botg && p.early_bot;
+    unsigned char* const tail = early ? smem + fb_tail_offset(HW, p.W, NT) : nullptr;
+    if (early) {
         __syncthreads();
-        bot_setup_workgroup<NT>(p, smem, smem + fb_tail_offset(HW, p.W, NT), L.wall, L.ballot);
+        bot_setup_workgroup<NT>(p, smem, tail, L.wall, L.ballot);
         __syncthreads();
-        if (threadIdx.x < 64) {
-            __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
-            bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, smem + fb_tail_offset(HW, p.W, NT), L.wall,
-                                 true);
-        }
-        else
-            emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, 64, early_cnt);
-        return;
     }
-    emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0);
-    if (FB && botg && threadIdx.x < 64)   // every read of the stored state is behind phase A's barrier
-        bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2);   // the step's arrays are dead: only L.outw is read on
+    if (!early || threadIdx.x >= 64) emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0, early ? early_cnt : nullptr);
+    if (FB && botg && threadIdx.x < 64) {
+        if (early) __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
+        bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, tail, early ? L.wall : nullptr, early);
+    }
 }
 
 // ---------------------------------------------------------------------------
