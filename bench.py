@@ -68,6 +68,10 @@ def parse():
                          "share one GPU, as tests/test_gpu_shard.py does)")
     ap.add_argument("--bucket-streams", type=int, default=0, choices=[0, 1],
                     help="mixed workload: 1 = each size bucket on its own HIP stream (concurrent), 0 = back to back")
+    ap.add_argument("--group-policy", default="default",
+                    help="mixed workload: the buckets' steps in one mrts_step_group call with this policy "
+                         "(MRTS_GROUP_* bits, include/microrts_amd.h; default = merge-fit | bots-first), "
+                         "or 'none' = one step launch per bucket")
     ap.add_argument("--dump", default=None,
                     help="save each rank's final obs / masks / raw rewards / dones to DUMP.rank<r>.npz (shard tests)")
     return ap.parse_args()
@@ -150,7 +154,9 @@ def run_mixed(args, rank, dev):
         nb = int(n * frac) // 4 * 4
         bots = [microrts_ai.workerRushAI] * (nb // 4) + [microrts_ai.coacAI] * (nb // 4)
         buckets.append(dict(map_paths=[m], num_selfplay_envs=nb // 2, num_bot_envs=len(bots), ai2s=bots))
-    env = MicroRTSMixedMapVecEnv(buckets, concurrent=bool(args.bucket_streams), max_steps=args.max_steps, device=dev,
+    gp = args.group_policy
+    gp = None if gp == "none" else gp if gp == "default" else int(gp)
+    env = MicroRTSMixedMapVecEnv(buckets, concurrent=bool(args.bucket_streams), group_policy=gp, max_steps=args.max_steps, device=dev,
                                  return_tensors=True,
                                  reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), eager_masks=not args.no_eager_masks)
     lib = _native.lib()
@@ -203,6 +209,7 @@ def run_mixed(args, rank, dev):
     stats = window_stats(before, after, args.steps)
     stats["buckets"] = buckets
     stats["buckets_concurrent"] = env.concurrent
+    stats["group_policy"] = env.group_policy if env.grouped else None
     if ev.get("all"):
         stats["step_all_buckets_ms"] = float(np.mean([a.elapsed_time(b) for a, b in ev["all"]]))
     return elapsed, {}, env.error_flags(), 256, sum(e._n_games() for e in env.envs), env.num_envs, 29, 0, stats
@@ -561,11 +568,11 @@ def main():
                     "traffic_bytes_per_launch": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": kb[dom], "kernel": dom, "avg_launch_ms": round(kern[dom], 4)}
         bk = stats.get("buckets")
-        if bk and all(b["step_ms"] for b in bk):
+        if bk and (stats.get("step_all_buckets_ms") or all(b["step_ms"] for b in bk)):
             # configs[4]: one step kernel per size bucket -- the algorithmic bytes of all
             # buckets over the time their launches take together (concurrent streams:
             # the span from the first launch's start to the last one's end; back to back:
-            # the sum of their mean launch times)
+            # the sum of their mean launch times; one mrts_step_group call: its launches)
             tb = sum(b["step_bytes"] for b in bk)
             tms = stats.get("step_all_buckets_ms") or sum(b["step_ms"] for b in bk)
             achieved = tb / (tms * 1e-3) / 1e9

@@ -153,6 +153,34 @@ int mrts_set_reward_weight(mrts_vec *h, const double *weight6, int32_t reward_sh
 int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs,
                        double *raw_reward, uint8_t *done, double *reward, uint8_t *done0);
 
+/* One step of several engines -- the map-size buckets of one mixed batch --
+ * equivalent to mrts_step (io[i].reward == NULL) or mrts_step_weighted on each
+ * hs[i] in order on `stream`.  Replaces the sequence of
+ * JNIGridnetVecClient.gameStep calls that one reference vec env per map size
+ * makes (vec_env.py:148-150: one size per env; vec_env.py:986-1003: gameStep),
+ * so that engines whose kernels share planes, obs dtype and bot fusion run in
+ * one kernel launch instead of one each.  policy: MRTS_GROUP_SEPARATE (one
+ * launch per engine), MRTS_GROUP_MERGE_FIT (merge members that still fit
+ * >= 4 workgroups per CU at the launch's LDS size; larger maps keep their own
+ * launch), MRTS_GROUP_MERGE_ALL (every compatible member), | MRTS_GROUP_BOTS_FIRST
+ * (bot games start before selfplay games in the merged grid).  Outputs are the
+ * same bytes whatever the policy.  1 <= n <= MRTS_STEP_GROUP_MAX, each handle once. */
+#define MRTS_STEP_GROUP_MAX 4
+#define MRTS_GROUP_SEPARATE 0
+#define MRTS_GROUP_MERGE_FIT 1
+#define MRTS_GROUP_MERGE_ALL 2
+#define MRTS_GROUP_BOTS_FIRST 4
+typedef struct mrts_step_io {
+    const int64_t *actions;
+    const int32_t *source;
+    void *obs;
+    double *raw_reward;
+    uint8_t *done;
+    double *reward;   /* NULL: mrts_step's outputs only */
+    uint8_t *done0;
+} mrts_step_io;
+int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy);
+
 /* Map cycling (vec_env.py:1038-1056): reset `count` games (host arrays) onto
  * the given map indices and rewrite their envs' obs; parked games play again. */
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);

@@ -6,6 +6,7 @@
 // and kernel dispatch.  No torch types cross this boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -417,18 +418,34 @@ int mrts_get_masks(mrts_vec *h, void *stream, int32_t *mask, int32_t *source) {
     return e ? hip_fail(h, e, "masks launch") : MRTS_OK;
 }
 
-int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs, double *raw_reward,
-              uint8_t *done) {
-    if (!bound(h) || !actions || !source || !obs || !raw_reward || !done)
-        return fail(h, MRTS_ESTATE, "step: workspace not bound or null buffer");
+// the step's parameters of one engine (mrts_step / mrts_step_weighted / mrts_step_group)
+static EngineParams step_params(const mrts_vec *h, const mrts_step_io &io) {
     EngineParams p = h->base;
-    p.actions = actions;
-    p.src = source;
-    p.obs = obs;
-    p.raw_reward = raw_reward;
-    p.done = done;
+    p.actions = io.actions;
+    p.src = io.source;
+    p.obs = io.obs;
+    p.raw_reward = io.raw_reward;
+    p.done = io.done;
+    if (io.reward) {
+        p.reward = io.reward;
+        p.done0 = io.done0;
+        for (int k = 0; k < 6; k++) p.rw[k] = h->rw[k];
+        p.shaping = h->shaping;
+    }
     p.mask = h->next_mask;
     p.src_out = h->next_src;
+    return p;
+}
+
+static bool io_ok(const mrts_step_io &io, bool weighted) {
+    return io.actions && io.source && io.obs && io.raw_reward && io.done && (!weighted || (io.reward && io.done0));
+}
+
+int mrts_step(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs, double *raw_reward,
+              uint8_t *done) {
+    const mrts_step_io io{actions, source, obs, raw_reward, done, nullptr, nullptr};
+    if (!bound(h) || !io_ok(io, false)) return fail(h, MRTS_ESTATE, "step: workspace not bound or null buffer");
+    EngineParams p = step_params(h, io);
     hipError_t e = step_launch(h, p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
 }
@@ -448,22 +465,68 @@ int mrts_set_reward_weight(mrts_vec *h, const double *w, int32_t shaping) {
 
 int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const int32_t *source, void *obs,
                        double *raw_reward, uint8_t *done, double *reward, uint8_t *done0) {
-    if (!bound(h) || !actions || !source || !obs || !raw_reward || !done || !reward || !done0)
-        return fail(h, MRTS_ESTATE, "step_weighted: workspace not bound or null buffer");
-    EngineParams p = h->base;
-    p.actions = actions;
-    p.src = source;
-    p.obs = obs;
-    p.raw_reward = raw_reward;
-    p.done = done;
-    p.reward = reward;
-    p.done0 = done0;
-    for (int k = 0; k < 6; k++) p.rw[k] = h->rw[k];
-    p.shaping = h->shaping;
-    p.mask = h->next_mask;
-    p.src_out = h->next_src;
+    const mrts_step_io io{actions, source, obs, raw_reward, done, reward, done0};
+    if (!bound(h) || !io_ok(io, true)) return fail(h, MRTS_ESTATE, "step_weighted: workspace not bound or null buffer");
+    EngineParams p = step_params(h, io);
     hipError_t e = step_launch(h, p, (hipStream_t)stream);
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
+}
+
+// A member may share a launch when its workgroup still leaves >= 4 per CU at the
+// widest workgroup size (a larger map -- 24x24 fused: 52 KB -- keeps its own
+// launch, or it would cut every member's residency to its own).
+static const size_t kGroupLdsCap = 163840 / 4;
+
+int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy) {
+    if (!hs || !io || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(nullptr, MRTS_EINVAL, "step_group: bad arguments");
+    for (int i = 0; i < n; i++) {
+        if (!bound(hs[i]) || !io_ok(io[i], io[i].reward != nullptr))
+            return fail(hs[i], MRTS_ESTATE, "step_group: workspace not bound or null buffer");
+        for (int j = 0; j < i; j++)
+            if (hs[j] == hs[i]) return fail(hs[i], MRTS_EINVAL, "step_group: an engine listed twice");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const int merge = policy & 3;
+    EngineParams ps[MRTS_STEP_GROUP_MAX];
+    for (int i = 0; i < n; i++) {
+        mrts_vec *h = hs[i];
+        ps[i] = step_params(h, io[i]);
+        // the tick's bot decisions, when an earlier launch did not make them
+        hipError_t e = h->bots_ready ? hipSuccess : mrts_engine_bots(&ps[i], s);
+        if (e) return hip_fail(h, e, "step_group bot launch");
+        ps[i].fuse_bots = fused(h) ? 1 : 0;
+    }
+    // launches: members of equal planes / obs type / fusion together (merge != 0),
+    // each at most once, in the caller's order of their first member
+    bool done[MRTS_STEP_GROUP_MAX] = {};
+    for (int i = 0; i < n; i++) {
+        if (done[i]) continue;
+        EngineParams grp[MRTS_STEP_GROUP_MAX];
+        int m = 0;
+        auto lds = [&](const EngineParams &p, int NT) { return mrts_engine_group_lds_bytes(p.HW, p.W, p.fuse_bots, NT); };
+        auto compatible = [&](const EngineParams &a, const EngineParams &b) {
+            return a.partial_obs == b.partial_obs && a.obs_float == b.obs_float && (a.fuse_bots != 0) == (b.fuse_bots != 0);
+        };
+        grp[m++] = ps[i];
+        done[i] = true;
+        for (int j = i + 1; merge && j < n; j++) {
+            if (done[j] || !compatible(ps[i], ps[j])) continue;
+            int NT = mrts_engine_step_nt(ps[j].HW, ps[j].fuse_bots);
+            for (int k = 0; k < m; k++) NT = std::max(NT, mrts_engine_step_nt(grp[k].HW, grp[k].fuse_bots));
+            bool fits = true;
+            if (merge == MRTS_GROUP_MERGE_FIT) {
+                fits = lds(ps[j], NT) <= kGroupLdsCap;
+                for (int k = 0; k < m; k++) fits = fits && lds(grp[k], NT) <= kGroupLdsCap;
+            }
+            if (!fits) continue;
+            grp[m++] = ps[j];
+            done[j] = true;
+        }
+        hipError_t e = mrts_engine_step_group(grp, m, s, (policy & MRTS_GROUP_BOTS_FIRST) != 0);
+        if (e) return hip_fail(hs[i], e, "step_group launch");
+    }
+    for (int i = 0; i < n; i++) hs[i]->bots_ready = ps[i].fuse_bots != 0;
+    return MRTS_OK;
 }
 
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs) {

@@ -43,10 +43,25 @@ struct EngineParams {
 };
 __device__ __forceinline__ bool game_parked(const EngineParams &p, int g) { return p.parked && p.parked[g]; }
 
+// The step kernel's argument: the engines of one launch and the grid's segments
+// (workgroups seg_block[k] .. seg_block[k + 1] - 1 run games seg_game[k].. of
+// engine e[seg_member[k]]).
+#define MRTS_STEP_GROUP_MAX 4
+struct StepGroup {
+    EngineParams e[MRTS_STEP_GROUP_MAX];
+    int seg_block[2 * MRTS_STEP_GROUP_MAX + 1];
+    int seg_member[2 * MRTS_STEP_GROUP_MAX];
+    int seg_game[2 * MRTS_STEP_GROUP_MAX];
+    int nseg;
+};
+
 extern "C" {
 hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t *games, const int32_t *maps, int count);
 hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
+hipError_t mrts_engine_step_group(const EngineParams *ps, int n, hipStream_t s, int bots_first);
+size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT);
+int mrts_engine_step_nt(int HW, int fused);
 hipError_t mrts_engine_bots(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *raw);
 hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);

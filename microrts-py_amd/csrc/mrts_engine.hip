@@ -862,8 +862,8 @@ __device__ __forceinline__ void commit_game(const EngineParams& p, const Lds& L,
 // FB (bot fusion, p.fuse_bots): in a bot game's workgroup, wave 0 decides the
 // NEXT tick's bot actions (bots::bot_game on the state just stored) while waves
 // 1.. stream this tick's outputs; its LDS follows the step's (launch_all).
-template <int NT, int P, typename OT, bool FB = false>
-__global__ __launch_bounds__(NT) void k_step(EngineParams p) {
+template <int NT, int P, typename OT, bool FB>
+__device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
     Lds L = carve(smem, HW, p.W, NT);
@@ -877,7 +877,6 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     const Grid gd{p.W, p.H, HW};
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
-    const int g = blockIdx.x;
     if (game_parked(p, g)) return;   // no tick: its outputs stay zero (mrts_park_games)
     if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
     if (FB && P == 29 && p.early_bot && g >= p.nsp_games && NT > 64) {   // the early bot's tail arrays start zeroed
@@ -1192,6 +1191,20 @@ __global__ __launch_bounds__(NT) void k_step(EngineParams p) {
     }
 }
 
+// One step launch over the games of one or more engines (map-size buckets of one
+// batch, mrts_step_group): the grid is cut into segments of consecutive games of
+// one engine; a workgroup finds its segment with a scalar scan of the table (at
+// most 2 * MRTS_STEP_GROUP_MAX entries) and runs that engine's game.  Each
+// engine's arrays, map size and LDS carve are its own; the launch's dynamic LDS
+// is the largest member's.  A single engine is a one-member, one-segment group.
+template <int NT, int P, typename OT, bool FB = false>
+__global__ __launch_bounds__(NT) void k_step(const StepGroup sg) {
+    const int b = blockIdx.x;
+    int k = 0;
+    while (k + 1 < sg.nseg && b >= sg.seg_block[k + 1]) k++;
+    step_game<NT, P, OT, FB>(sg.e[sg.seg_member[k]], sg.seg_game[k] + (b - sg.seg_block[k]));
+}
+
 // ---------------------------------------------------------------------------
 // render("rgb_array") (vec_env.py:1075-1084): a size x size RGB frame of one
 // game, one lane per pixel.  The Java PhysicalGameStatePanel is absent, so the
@@ -1485,9 +1498,34 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
 // launchers
 
 
-template <typename K>
-static void launch_step(K kernel, int NT, size_t sh, hipStream_t s, const EngineParams& p) {
-    hipLaunchKernelGGL(kernel, dim3(p.G), dim3(NT), sh, s, p);
+static StepGroup one_engine(const EngineParams& p) {
+    StepGroup sg{};
+    sg.e[0] = p;
+    sg.seg_block[1] = p.G;
+    sg.nseg = 1;
+    return sg;
+}
+
+// the step kernel of a launch's (planes, obs type, bot fusion)
+template <int NT>
+static void launch_step(const StepGroup& sg, int grid, size_t sh, hipStream_t s, bool partial, bool fl, bool fb) {
+    if (fb) {
+        if (partial) {
+            if (fl) hipLaunchKernelGGL((k_step<NT, 31, float, true>), dim3(grid), dim3(NT), sh, s, sg);
+            else hipLaunchKernelGGL((k_step<NT, 31, int32_t, true>), dim3(grid), dim3(NT), sh, s, sg);
+        } else {
+            if (fl) hipLaunchKernelGGL((k_step<NT, 29, float, true>), dim3(grid), dim3(NT), sh, s, sg);
+            else hipLaunchKernelGGL((k_step<NT, 29, int32_t, true>), dim3(grid), dim3(NT), sh, s, sg);
+        }
+    } else {
+        if (partial) {
+            if (fl) hipLaunchKernelGGL((k_step<NT, 31, float>), dim3(grid), dim3(NT), sh, s, sg);
+            else hipLaunchKernelGGL((k_step<NT, 31, int32_t>), dim3(grid), dim3(NT), sh, s, sg);
+        } else {
+            if (fl) hipLaunchKernelGGL((k_step<NT, 29, float>), dim3(grid), dim3(NT), sh, s, sg);
+            else hipLaunchKernelGGL((k_step<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, sg);
+        }
+    }
 }
 
 template <int NT>
@@ -1506,23 +1544,10 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
         }
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
-    } else if (p.fuse_bots && NT > 64) {
-        sh = fb_lds_bytes(p.HW, p.W, NT);
-        if (p.partial_obs) {
-            if (p.obs_float) launch_step(k_step<NT, 31, float, true>, NT, sh, s, p);
-            else launch_step(k_step<NT, 31, int32_t, true>, NT, sh, s, p);
-        } else {
-            if (p.obs_float) launch_step(k_step<NT, 29, float, true>, NT, sh, s, p);
-            else launch_step(k_step<NT, 29, int32_t, true>, NT, sh, s, p);
-        }
     } else {
-        if (p.partial_obs) {
-            if (p.obs_float) launch_step(k_step<NT, 31, float>, NT, sh, s, p);
-            else launch_step(k_step<NT, 31, int32_t>, NT, sh, s, p);
-        } else {
-            if (p.obs_float) launch_step(k_step<NT, 29, float>, NT, sh, s, p);
-            else launch_step(k_step<NT, 29, int32_t>, NT, sh, s, p);
-        }
+        const bool fb = p.fuse_bots && NT > 64;
+        if (fb) sh = fb_lds_bytes(p.HW, p.W, NT);
+        launch_step<NT>(one_engine(p), grid, sh, s, p.partial_obs, p.obs_float, fb);
     }
     return hipGetLastError();
 }
@@ -1537,6 +1562,54 @@ static hipError_t dispatch(const EngineParams& p, int kind, hipStream_t s, const
     if (p.HW <= 64) return launch_all<64>(p, kind, s, games, maps, count);
     if (p.HW <= 128) return launch_all<128>(p, kind, s, games, maps, count);
     return launch_all<256>(p, kind, s, games, maps, count);
+}
+
+// One step launch over n engines of equal planes, obs type and bot fusion, at the
+// widest member's workgroup size (a narrower map leaves lanes idle in the game
+// logic; every wave still streams outputs).  bots_first: every member's bot games
+// take the grid's first segments, then the selfplay games -- workgroups start in
+// grid order, so the longest chains (the fused bot after the tick) start first and
+// the short selfplay games fill the last round.
+static hipError_t step_group(const EngineParams* ps, int n, hipStream_t s, bool bots_first) {
+    if (n < 1 || n > MRTS_STEP_GROUP_MAX) return hipErrorInvalidValue;
+    const EngineParams& p0 = ps[0];
+    const bool fused = p0.fuse_bots != 0;
+    int NT = 64;
+    for (int i = 0; i < n; i++) {
+        const EngineParams& p = ps[i];
+        if (p.partial_obs != p0.partial_obs || p.obs_float != p0.obs_float || (p.fuse_bots != 0) != fused) return hipErrorInvalidValue;
+        NT = std::max(NT, step_nt(p.HW, fused));
+    }
+    StepGroup sg{};
+    size_t sh = 0;
+    for (int i = 0; i < n; i++) {
+        EngineParams& e = sg.e[i];
+        e = ps[i];
+        if (fused) e.early_bot = early_bot_disjoint(e.HW, e.W, NT) ? 1 : 0;   // the layout at this launch's NT
+        sh = std::max(sh, fused ? fb_lds_bytes(e.HW, e.W, NT) : lds_bytes(e.HW, e.W, NT));
+    }
+    int grid = 0;
+    auto seg = [&](int m, int g0, int g1) {
+        if (g1 <= g0) return;
+        sg.seg_block[sg.nseg] = grid;
+        sg.seg_member[sg.nseg] = m;
+        sg.seg_game[sg.nseg] = g0;
+        sg.nseg++;
+        grid += g1 - g0;
+    };
+    for (int pass = 0; pass < (bots_first ? 2 : 1); pass++)
+        for (int i = 0; i < n; i++) {
+            const EngineParams& e = sg.e[i];
+            if (!bots_first) seg(i, 0, e.G);
+            else if (pass == 0) seg(i, e.nsp_games, e.G);
+            else seg(i, 0, e.nsp_games);
+        }
+    sg.seg_block[sg.nseg] = grid;
+    if (grid == 0) return hipSuccess;
+    if (NT == 64) launch_step<64>(sg, grid, sh, s, p0.partial_obs, p0.obs_float, false);
+    else if (NT == 128) launch_step<128>(sg, grid, sh, s, p0.partial_obs, p0.obs_float, fused);
+    else launch_step<256>(sg, grid, sh, s, p0.partial_obs, p0.obs_float, fused);
+    return hipGetLastError();
 }
 
 }  // namespace mrts
@@ -1555,6 +1628,13 @@ hipError_t mrts_engine_raw_obs(const EngineParams* p, hipStream_t s, int32_t* ra
     return hipGetLastError();
 }
 hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 2, s, nullptr, nullptr, 0); }
+hipError_t mrts_engine_step_group(const EngineParams* ps, int n, hipStream_t s, int bots_first) {
+    return mrts::step_group(ps, n, s, bots_first != 0);
+}
+size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT) {
+    return fused ? mrts::fb_lds_bytes(HW, W, NT) : mrts::lds_bytes(HW, W, NT);
+}
+int mrts_engine_step_nt(int HW, int fused) { return mrts::step_nt(HW, fused != 0); }
 hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
     int total = n * hw;
     if (total == 0) return hipSuccess;

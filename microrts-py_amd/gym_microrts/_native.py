@@ -64,8 +64,18 @@ class Info(ctypes.Structure):
     ]
 
 
-# every entry point of include/microrts_amd.h: (restype, argtypes)
 P = ctypes.c_void_p
+
+
+class StepIO(ctypes.Structure):
+    """mrts_step_io: one engine's buffers of an mrts_step_group call."""
+    _fields_ = [("actions", P), ("source", P), ("obs", P), ("raw_reward", P), ("done", P), ("reward", P), ("done0", P)]
+
+
+STEP_GROUP_MAX = 4
+GROUP_SEPARATE, GROUP_MERGE_FIT, GROUP_MERGE_ALL, GROUP_BOTS_FIRST = 0, 1, 2, 4
+
+# every entry point of include/microrts_amd.h: (restype, argtypes)
 SIGNATURES = {
     "mrts_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.POINTER(P)]),
     "mrts_info": (ctypes.c_int, [P, ctypes.POINTER(Info)]),
@@ -76,6 +86,7 @@ SIGNATURES = {
     "mrts_get_raw_obs": (ctypes.c_int, [P, P, P]),
     "mrts_set_reward_weight": (ctypes.c_int, [P, P, ctypes.c_int32]),
     "mrts_step_weighted": (ctypes.c_int, [P, P, P, P, P, P, P, P, P]),
+    "mrts_step_group": (ctypes.c_int, [P, ctypes.c_int32, P, P, ctypes.c_int32]),
     "mrts_reset_games": (ctypes.c_int, [P, P, P, P, ctypes.c_int32, P]),
     "mrts_add_map": (ctypes.c_int, [P, P, ctypes.c_char_p, P]),
     "mrts_park_games": (ctypes.c_int, [P, P, P, ctypes.c_int32, P]),

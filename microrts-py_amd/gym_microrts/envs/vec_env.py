@@ -462,13 +462,7 @@ class MicroRTSGridModeVecEnv:
             self._launch("step", _native.lib().mrts_step_weighted, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
                          self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr(), self._rew.data_ptr(),
                          self._done0.data_ptr())
-            raw = self._raw
-            if not self.reward_shaping:
-                raw = raw.clone()
-                raw[:, 1:] = 0
-            if len(self.cycle_maps) > self._cycle_min:
-                self._cycle(self._done0.cpu().numpy())
-            return self._obs, self._rew, self._done0, LazyInfos(raw)
+            return self._tensor_outputs()
         self._launch("step", _native.lib().mrts_step, self._h, self._stream(), a.data_ptr(), self._src.data_ptr(),
                      self._obs.data_ptr(), self._raw.data_ptr(), self._done.data_ptr())
         self._mask_prefetch = None
@@ -499,6 +493,25 @@ class MicroRTSGridModeVecEnv:
                 self._sync()
         infos = [{"raw_rewards": item} for item in reward]
         return obs, reward @ self.reward_weight, done[:, 0], infos
+
+    def _step_io(self):
+        """The tensor contract's step buffers (mrts_step_io) after step_async, for a
+        step launched by mrts_step_group (MicroRTSMixedMapVecEnv); _tensor_outputs()
+        afterwards returns what step_wait would."""
+        if not self._mask_fresh:
+            self.get_action_mask()
+        self._mask_fresh = self.eager_masks
+        return _native.StepIO(self._actions_in.data_ptr(), self._src.data_ptr(), self._obs.data_ptr(), self._raw.data_ptr(),
+                              self._done.data_ptr(), self._rew.data_ptr(), self._done0.data_ptr())
+
+    def _tensor_outputs(self):
+        raw = self._raw
+        if not self.reward_shaping:
+            raw = raw.clone()
+            raw[:, 1:] = 0
+        if len(self.cycle_maps) > self._cycle_min:
+            self._cycle(self._done0.cpu().numpy())
+        return self._obs, self._rew, self._done0, LazyInfos(raw)
 
     def game_of_env(self, e):
         """env index -> game index (selfplay pairs 2k / 2k+1 share game k, then bot envs)."""
@@ -754,7 +767,7 @@ class MicroRTSMixedMapVecEnv:
       obs, rew, done, infos = env.step(actions)  # actions: list over buckets
     """
 
-    def __init__(self, buckets, concurrent=False, **common):
+    def __init__(self, buckets, concurrent=False, group_policy="default", **common):
         self.envs = []
         for b in buckets:
             kw = dict(common)
@@ -773,6 +786,14 @@ class MicroRTSMixedMapVecEnv:
         # (configs[4] 22.6 vs 23.8 M env-steps/s, profiles/r02i/)
         self.concurrent = bool(concurrent) and len(self.envs) > 1
         self._streams = [torch.cuda.Stream(device=e.device) for e in self.envs] if self.concurrent else None
+        # group_policy (tensor contract, no map cycling, <= 4 buckets): every bucket's
+        # step in one mrts_step_group call -- buckets whose kernels fit one launch
+        # share it (include/microrts_amd.h MRTS_GROUP_*); None = one step_wait per bucket
+        if group_policy == "default":
+            group_policy = _native.GROUP_MERGE_FIT | _native.GROUP_BOTS_FIRST
+        self.group_policy = group_policy
+        self.grouped = (group_policy is not None and not self.concurrent and 1 < len(self.envs) <= _native.STEP_GROUP_MAX
+                        and all(e.contract == "tensors" and len(e.cycle_maps) <= e._cycle_min for e in self.envs))
 
     def reset(self):
         return [e.reset() for e in self.envs]
@@ -786,6 +807,15 @@ class MicroRTSMixedMapVecEnv:
             e.step_async(a)
 
     def step_wait(self):
+        if self.grouped:
+            import ctypes
+
+            io = (_native.StepIO * len(self.envs))(*[e._step_io() for e in self.envs])
+            hs = (ctypes.c_void_p * len(self.envs))(*[e._h for e in self.envs])
+            e0 = self.envs[0]
+            e0._launch("step", _native.lib().mrts_step_group, hs, len(self.envs), e0._stream(), io, self.group_policy)
+            outs = [e._tensor_outputs() for e in self.envs]
+            return tuple(list(x) for x in zip(*outs))
         if not self.concurrent:
             outs = [e.step_wait() for e in self.envs]
             return tuple(list(x) for x in zip(*outs))

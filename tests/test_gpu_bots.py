@@ -166,29 +166,24 @@ def test_league_outcomes_on_device():
     assert g.error_flags() == 0
 
 
-@pytest.mark.parametrize("concurrent", [False, True])
-def test_mixed_map_buckets_match_oracle(concurrent):
-    """BASELINE configs[4]: 8x8 / 16x16 / 24x24 buckets in one MicroRTSMixedMapVecEnv,
-    selfplay + device workerRush / coacAI envs, every bucket bit-exact vs its oracle
-    (buckets back to back, and each on its own HIP stream)."""
+def mixed_lockstep(spec, steps, max_steps=300, partial_obs=False, **kw):
+    """MicroRTSMixedMapVecEnv (kw: concurrent / group_policy) vs one oracle per bucket:
+    obs, masks, rewards and dones bit-exact every step."""
     import torch
 
     from gym_microrts import microrts_ai
     from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
     from oracle_py import OracleVecEnv, sample_actions
 
-    spec = [("maps/8x8/basesWorkers8x8.xml", 8, ["workerRushAI", "coacAI"] * 2),
-            ("maps/16x16/basesWorkers16x16.xml", 16, ["coacAI", "workerRushAI", "randomBiasedAI", "lightRushAI"] * 2),
-            ("maps/24x24/basesWorkers24x24.xml", 4, ["workerRushAI", "coacAI"])]
     w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
     env = MicroRTSMixedMapVecEnv([dict(map_paths=[m], num_selfplay_envs=nsp, ai2s=[getattr(microrts_ai, a) for a in ais])
-                                  for m, nsp, ais in spec], concurrent=concurrent, max_steps=300, return_tensors=True,
-                                 reward_weight=w, obs_dtype=torch.int32)
-    orc = [OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, m)], max_steps=300, ai2s=ais, reward_weight=w)
-           for m, nsp, ais in spec]
+                                  for m, nsp, ais in spec], max_steps=max_steps, return_tensors=True, partial_obs=partial_obs,
+                                 reward_weight=w, obs_dtype=torch.int32, **kw)
+    orc = [OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, m)], max_steps=max_steps, ai2s=ais, reward_weight=w,
+                        partial_obs=partial_obs) for m, nsp, ais in spec]
     for og, oo in zip(env.reset(), [o.reset() for o in orc]):
         np.testing.assert_array_equal(og.cpu().numpy(), oo)
-    for s in range(400):
+    for s in range(steps):
         masks = env.get_action_mask()
         acts = []
         for mg, o in zip(masks, orc):
@@ -199,8 +194,40 @@ def test_mixed_map_buckets_match_oracle(concurrent):
         for k, o in enumerate(orc):
             oo, ro, do, _ = o.step(acts[k])
             np.testing.assert_array_equal(obs[k].cpu().numpy(), oo, err_msg=f"bucket {k} step {s}")
+            np.testing.assert_array_equal(rew[k].cpu().numpy(), ro, err_msg=f"bucket {k} step {s}")
             np.testing.assert_array_equal(done[k].cpu().numpy(), do)
     assert env.error_flags() == 0
+    return env
+
+
+# group policies: None = one step_wait per bucket; else mrts_step_group's MRTS_GROUP_* bits
+# (1 merge-fit, 2 merge-all, | 4 bots first)
+@pytest.mark.parametrize("concurrent,group_policy", [(False, None), (True, None), (False, 0), (False, 1 | 4), (False, 2),
+                                                     (False, 2 | 4)])
+def test_mixed_map_buckets_match_oracle(concurrent, group_policy):
+    """BASELINE configs[4]: 8x8 / 16x16 / 24x24 buckets in one MicroRTSMixedMapVecEnv,
+    selfplay + device workerRush / coacAI envs, every bucket bit-exact vs its oracle
+    (buckets back to back, each on its own HIP stream, and in one mrts_step_group
+    call: separate launches, 8x8 + 16x16 in one launch, all three in one)."""
+    spec = [("maps/8x8/basesWorkers8x8.xml", 8, ["workerRushAI", "coacAI"] * 2),
+            ("maps/16x16/basesWorkers16x16.xml", 16, ["coacAI", "workerRushAI", "randomBiasedAI", "lightRushAI"] * 2),
+            ("maps/24x24/basesWorkers24x24.xml", 4, ["workerRushAI", "coacAI"])]
+    env = mixed_lockstep(spec, 400, concurrent=concurrent, group_policy=group_policy)
+    assert env.grouped == (group_policy is not None)
+
+
+@pytest.mark.parametrize("partial_obs", [False, True])
+def test_step_group_walled_odd_sizes(partial_obs):
+    """mrts_step_group merging four map sizes of different cell counts into one
+    256-lane launch (merge-all, bots first): 8x8 and 10x10 games run on workgroups
+    wider than their maps, walled 15x15 and 9x13 maps (HW % 4 != 0) with the early
+    fused bot at the launch's width, bit-exact vs the oracle per bucket."""
+    spec = [("maps/8x8/basesWorkers8x8.xml", 4, ["coacAI", "lightRushAI"]),
+            ("maps/10x10/basesTwoWorkers10x10.xml", 2, ["workerRushAI", "randomBiasedAI"]),
+            ("maps/15x15/basesWorkersWalls15x15.xml", 4, ["coacAI", "workerRushAI", "lightRushAI"]),
+            ("maps/9x13/basesWorkersWalls9x13.xml", 2, ["coacAI", "randomBiasedAI"])]
+    env = mixed_lockstep(spec, 300, max_steps=200, partial_obs=partial_obs, group_policy=2 | 4)
+    assert env.grouped
 
 
 def test_bots_without_fusion():
