@@ -210,6 +210,7 @@ def run_mixed(args, rank, dev):
     stats["buckets"] = buckets
     stats["buckets_concurrent"] = env.concurrent
     stats["group_policy"] = env.group_policy if env.grouped else None
+    stats["bucket_launch"], stats["launches_per_step"] = env.launch_plan()
     if ev.get("all"):
         stats["step_all_buckets_ms"] = float(np.mean([a.elapsed_time(b) for a, b in ev["all"]]))
     return elapsed, {}, env.error_flags(), 256, sum(e._n_games() for e in env.envs), env.num_envs, 29, 0, stats
@@ -576,9 +577,17 @@ def main():
             tb = sum(b["step_bytes"] for b in bk)
             tms = stats.get("step_all_buckets_ms") or sum(b["step_ms"] for b in bk)
             achieved = tb / (tms * 1e-3) / 1e9
+            # PMC: the step kernel's mean bytes per launch x launches per step (each
+            # step makes every launch of the group's plan once)
+            nl = stats.get("launches_per_step") or len(bk)
+            default_cmd = args.api == "tensor" and eager and args.sampler == "src" and args.group_policy == "default"
+            traffic, tsrc = pmc_traffic("step", f"{args.workload}@{N}") if default_cmd else (None, "non-default bench options")
+            traffic = None if traffic is None else traffic * nl
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": tb,
-                    "kernel": "step (all size buckets)", "avg_launch_ms": round(tms, 4)}
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None if traffic is None else round(traffic / (tms * 1e-3) / 1e9, 1),
+                    "traffic_bytes_per_step": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": tb,
+                    "kernel": "step (all size buckets)", "launches": nl, "avg_launch_ms": round(tms, 4)}
         wc = stats.get("box_write_ceiling")
         if roof and wc and roof.get("kernel") == "step":
             roof["frac_of_box_write_ceiling"] = round(roof["achieved"] / wc["GBps"], 4)

@@ -181,6 +181,11 @@ typedef struct mrts_step_io {
 } mrts_step_io;
 int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy);
 
+/* The launches mrts_step_group(hs, n, ..., policy) would make now: launch_of[i] =
+ * the launch (0 ..) engine i runs in, *launches = their number.  No reference
+ * counterpart (an engine-internal schedule, for profiling and tests). */
+int mrts_step_group_plan(mrts_vec *const *hs, int32_t n, int32_t policy, int32_t *launch_of, int32_t *launches);
+
 /* Map cycling (vec_env.py:1038-1056): reset `count` games (host arrays) onto
  * the given map indices and rewrite their envs' obs; parked games play again. */
 int mrts_reset_games(mrts_vec *h, void *stream, const int32_t *games, const int32_t *maps, int32_t count, void *obs);

@@ -477,16 +477,68 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
 // launch, or it would cut every member's residency to its own).
 static const size_t kGroupLdsCap = 163840 / 4;
 
-int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy) {
-    if (!hs || !io || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(nullptr, MRTS_EINVAL, "step_group: bad arguments");
+// Launch plan of a group: launch_of[i] = the launch (0, 1, ..) member i runs in.
+// Members of equal planes / obs type / fusion share a launch (merge != 0), each
+// launch in the caller's order of its first member.  Returns the launch count.
+static int group_plan(const EngineParams *ps, int n, int policy, int *launch_of) {
+    const int merge = policy & 3;
+    auto lds = [&](const EngineParams &p, int NT) { return mrts_engine_group_lds_bytes(p.HW, p.W, p.fuse_bots, NT); };
+    auto compatible = [&](const EngineParams &a, const EngineParams &b) {
+        return a.partial_obs == b.partial_obs && a.obs_float == b.obs_float && (a.fuse_bots != 0) == (b.fuse_bots != 0);
+    };
+    for (int i = 0; i < n; i++) launch_of[i] = -1;
+    int nl = 0;
     for (int i = 0; i < n; i++) {
-        if (!bound(hs[i]) || !io_ok(io[i], io[i].reward != nullptr))
+        if (launch_of[i] >= 0) continue;
+        int NT = mrts_engine_step_nt(ps[i].HW, ps[i].fuse_bots);
+        launch_of[i] = nl;
+        for (int j = i + 1; merge && j < n; j++) {
+            if (launch_of[j] >= 0 || !compatible(ps[i], ps[j])) continue;
+            const int NT2 = std::max(NT, mrts_engine_step_nt(ps[j].HW, ps[j].fuse_bots));
+            bool fits = true;
+            if (merge == MRTS_GROUP_MERGE_FIT)
+                for (int k = 0; k < n; k++)
+                    if ((k == j || launch_of[k] == nl) && lds(ps[k], NT2) > kGroupLdsCap) fits = false;
+            if (!fits) continue;
+            launch_of[j] = nl;
+            NT = NT2;
+        }
+        nl++;
+    }
+    return nl;
+}
+
+static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io) {
+    if (!hs || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(nullptr, MRTS_EINVAL, "step_group: bad arguments");
+    for (int i = 0; i < n; i++) {
+        if (!bound(hs[i]) || (io && !io_ok(io[i], io[i].reward != nullptr)))
             return fail(hs[i], MRTS_ESTATE, "step_group: workspace not bound or null buffer");
         for (int j = 0; j < i; j++)
             if (hs[j] == hs[i]) return fail(hs[i], MRTS_EINVAL, "step_group: an engine listed twice");
     }
+    return MRTS_OK;
+}
+
+int mrts_step_group_plan(mrts_vec *const *hs, int32_t n, int32_t policy, int32_t *launch_of, int32_t *launches) {
+    int rc = group_check(hs, n, nullptr);
+    if (rc) return rc;
+    if (!launch_of || !launches) return fail(hs[0], MRTS_EINVAL, "step_group_plan: null output");
+    EngineParams ps[MRTS_STEP_GROUP_MAX];
+    int lo[MRTS_STEP_GROUP_MAX];
+    for (int i = 0; i < n; i++) {
+        ps[i] = hs[i]->base;
+        ps[i].fuse_bots = fused(hs[i]) ? 1 : 0;
+    }
+    *launches = group_plan(ps, n, policy, lo);
+    for (int i = 0; i < n; i++) launch_of[i] = lo[i];
+    return MRTS_OK;
+}
+
+int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy) {
+    int rc = group_check(hs, n, io);
+    if (rc) return rc;
+    if (!io) return fail(hs[0], MRTS_EINVAL, "step_group: null io");
     hipStream_t s = (hipStream_t)stream;
-    const int merge = policy & 3;
     EngineParams ps[MRTS_STEP_GROUP_MAX];
     for (int i = 0; i < n; i++) {
         mrts_vec *h = hs[i];
@@ -496,34 +548,18 @@ int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_ste
         if (e) return hip_fail(h, e, "step_group bot launch");
         ps[i].fuse_bots = fused(h) ? 1 : 0;
     }
-    // launches: members of equal planes / obs type / fusion together (merge != 0),
-    // each at most once, in the caller's order of their first member
-    bool done[MRTS_STEP_GROUP_MAX] = {};
-    for (int i = 0; i < n; i++) {
-        if (done[i]) continue;
+    int launch_of[MRTS_STEP_GROUP_MAX];
+    const int nl = group_plan(ps, n, policy, launch_of);
+    for (int l = 0; l < nl; l++) {
         EngineParams grp[MRTS_STEP_GROUP_MAX];
-        int m = 0;
-        auto lds = [&](const EngineParams &p, int NT) { return mrts_engine_group_lds_bytes(p.HW, p.W, p.fuse_bots, NT); };
-        auto compatible = [&](const EngineParams &a, const EngineParams &b) {
-            return a.partial_obs == b.partial_obs && a.obs_float == b.obs_float && (a.fuse_bots != 0) == (b.fuse_bots != 0);
-        };
-        grp[m++] = ps[i];
-        done[i] = true;
-        for (int j = i + 1; merge && j < n; j++) {
-            if (done[j] || !compatible(ps[i], ps[j])) continue;
-            int NT = mrts_engine_step_nt(ps[j].HW, ps[j].fuse_bots);
-            for (int k = 0; k < m; k++) NT = std::max(NT, mrts_engine_step_nt(grp[k].HW, grp[k].fuse_bots));
-            bool fits = true;
-            if (merge == MRTS_GROUP_MERGE_FIT) {
-                fits = lds(ps[j], NT) <= kGroupLdsCap;
-                for (int k = 0; k < m; k++) fits = fits && lds(grp[k], NT) <= kGroupLdsCap;
+        int m = 0, first = -1;
+        for (int i = 0; i < n; i++)
+            if (launch_of[i] == l) {
+                if (first < 0) first = i;
+                grp[m++] = ps[i];
             }
-            if (!fits) continue;
-            grp[m++] = ps[j];
-            done[j] = true;
-        }
         hipError_t e = mrts_engine_step_group(grp, m, s, (policy & MRTS_GROUP_BOTS_FIRST) != 0);
-        if (e) return hip_fail(hs[i], e, "step_group launch");
+        if (e) return hip_fail(hs[first], e, "step_group launch");
     }
     for (int i = 0; i < n; i++) hs[i]->bots_ready = ps[i].fuse_bots != 0;
     return MRTS_OK;

@@ -87,6 +87,7 @@ SIGNATURES = {
     "mrts_set_reward_weight": (ctypes.c_int, [P, P, ctypes.c_int32]),
     "mrts_step_weighted": (ctypes.c_int, [P, P, P, P, P, P, P, P, P]),
     "mrts_step_group": (ctypes.c_int, [P, ctypes.c_int32, P, P, ctypes.c_int32]),
+    "mrts_step_group_plan": (ctypes.c_int, [P, ctypes.c_int32, ctypes.c_int32, P, P]),
     "mrts_reset_games": (ctypes.c_int, [P, P, P, P, ctypes.c_int32, P]),
     "mrts_add_map": (ctypes.c_int, [P, P, ctypes.c_char_p, P]),
     "mrts_park_games": (ctypes.c_int, [P, P, P, ctypes.c_int32, P]),

@@ -795,6 +795,20 @@ class MicroRTSMixedMapVecEnv:
         self.grouped = (group_policy is not None and not self.concurrent and 1 < len(self.envs) <= _native.STEP_GROUP_MAX
                         and all(e.contract == "tensors" and len(e.cycle_maps) <= e._cycle_min for e in self.envs))
 
+    def launch_plan(self):
+        """(launch index of each bucket, launches per step) of the grouped step
+        (mrts_step_group_plan); one launch per bucket when not grouped."""
+        if not self.grouped:
+            return list(range(len(self.envs))), len(self.envs)
+        import ctypes
+
+        n = len(self.envs)
+        hs = (ctypes.c_void_p * n)(*[e._h for e in self.envs])
+        lo, nl = (ctypes.c_int32 * n)(), ctypes.c_int32()
+        _native.check(_native.lib().mrts_step_group_plan(hs, n, self.group_policy, lo, ctypes.byref(nl)), self.envs[0]._h,
+                      "step_group_plan")
+        return list(lo), int(nl.value)
+
     def reset(self):
         return [e.reset() for e in self.envs]
 

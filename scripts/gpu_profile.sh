@@ -19,10 +19,16 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
 fi
 BENCH="bench.py --steps 100 --warmup 20 --no-cpu-baseline"
 COAC="bench.py --workload coac --envs-per-gpu 1024 --steps 300 --warmup 20 --no-cpu-baseline"
+MIXED="bench.py --workload mixed --steps 100 --warmup 20 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt" -o kt -- python3 $BENCH > "$O/bench_kt.json" 2> "$O/kt.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt_coac" -o kt -- python3 $COAC > "$O/bench_coac_kt.json" 2> "$O/kt_coac.err"
-for W in selfplay coac; do
-  if [ $W = selfplay ]; then CMD="$BENCH"; KEY=selfplay@8192; else CMD="$COAC"; KEY=coac@1024; fi
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/kt_mixed" -o kt -- python3 $MIXED > "$O/bench_mixed_kt.json" 2> "$O/kt_mixed.err"
+for W in selfplay coac mixed; do
+  case $W in
+    selfplay) CMD="$BENCH"; KEY=selfplay@8192;;
+    coac) CMD="$COAC"; KEY=coac@1024;;
+    mixed) CMD="$MIXED"; KEY=mixed@8192;;
+  esac
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$O/pmc_$W/fetch" -o fetch -- python3 $CMD --no-kernel-events > "$O/pmc_$W.fetch.json" 2> "$O/pmc_$W.fetch.err"
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$O/pmc_$W/write" -o write -- python3 $CMD --no-kernel-events > "$O/pmc_$W.write.json" 2> "$O/pmc_$W.write.err"
   python3 scripts/pmc_summary.py "$O/pmc_$W" "$O/pmc_latest.json" --workload $KEY --command "$CMD" > "$O/pmc_$W.txt"
