@@ -74,6 +74,13 @@ __device__ __forceinline__ void st16(void* dst, int a, int b, int c, int d) {
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// L.vis: both players' visibility words (phase A), and before that the ballot
+// words of the step's first compaction (one 8-B word per wave and NT cells)
+__host__ __device__ inline size_t vis_bytes(int HW, int NT) {
+    const size_t v = 8 * (size_t)(HW / 32 + 1), b = 8 * (size_t)((HW + NT - 1) / NT) * (NT / 64);
+    return v > b ? v : b;
+}
+
 __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     size_t b = 0;
     b += a16(4 * (size_t)HW) * 10; // unit uid act seq aux resv list prod blist blist0
@@ -82,7 +89,7 @@ __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     b += a16(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     b += a16(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     b += a16(4 * SC_WORDS);
-    b += a16(8 * (size_t)(HW / 32 + 1));
+    b += a16(vis_bytes(HW, NT));
     b += a16(8 * (size_t)((HW + 2 * W) / 32 + 1));
     return b;
 }
@@ -121,7 +128,7 @@ __host__ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT)
     L.ballot = (unsigned long long*)take(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     L.posbits = (uint32_t*)take(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     L.sc = (int*)take(4 * SC_WORDS);
-    L.vis = (uint32_t*)take(8 * (size_t)(HW / 32 + 1));
+    L.vis = (uint32_t*)take(vis_bytes(HW, NT));
     L.claim = (uint32_t*)take(8 * (size_t)((HW + 2 * W) / 32 + 1));
     return L;
 }
@@ -985,8 +992,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     // (the compaction's barrier orders the reservations, claims, SC_OVER and the
     // bot rows before everything below; L.prod is first read by issue_player, behind
     // the next compaction's barriers, so this one needs no trailing barrier and takes
-    // its ballot words from L.vis, free until phase A: HW / 4 + 8 >= the ceil(HW / NT)
-    // * NT / 8 bytes a compaction needs for every NT <= HW + 64)
+    // its ballot words from L.vis, free until phase A and sized for them: vis_bytes)
     int nprod = compact_cells<NT, false>(HW, [&](int c) {
         uint32_t a = L.act[c];
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
