@@ -299,3 +299,13 @@ def test_bot_fusion_toggled_mid_game():
     assert g.error_flags() == 0
     g.close()
     o.close()
+
+
+def test_step_group_tiny_map_in_wide_workgroup():
+    """A 4x4 bucket merged with a 16x16 one runs on 256-lane workgroups: the step's
+    first compaction then needs four ballot words in L.vis (vis_bytes), more than the
+    4x4 map's visibility words -- sized for both, bit-exact vs the oracle."""
+    spec = [("maps/4x4/baseTwoWorkers4x4.xml", 8, ["workerRushAI", "coacAI", "randomBiasedAI", "lightRushAI"]),
+            ("maps/16x16/basesWorkers16x16.xml", 4, ["coacAI", "workerRushAI"])]
+    env = mixed_lockstep(spec, 300, max_steps=120, group_policy=2 | 4)
+    assert env.launch_plan() == ([0, 0], 1)
