@@ -508,10 +508,11 @@ static int group_plan(const EngineParams *ps, int n, int policy, int *launch_of)
     return nl;
 }
 
-static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io) {
+static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io, bool need_bound = true) {
     if (!hs || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(nullptr, MRTS_EINVAL, "step_group: bad arguments");
     for (int i = 0; i < n; i++) {
-        if (!bound(hs[i]) || (io && !io_ok(io[i], io[i].reward != nullptr)))
+        if (!hs[i]) return fail(nullptr, MRTS_EINVAL, "step_group: null handle");
+        if ((need_bound && !bound(hs[i])) || (io && !io_ok(io[i], io[i].reward != nullptr)))
             return fail(hs[i], MRTS_ESTATE, "step_group: workspace not bound or null buffer");
         for (int j = 0; j < i; j++)
             if (hs[j] == hs[i]) return fail(hs[i], MRTS_EINVAL, "step_group: an engine listed twice");
@@ -520,13 +521,17 @@ static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io) {
 }
 
 int mrts_step_group_plan(mrts_vec *const *hs, int32_t n, int32_t policy, int32_t *launch_of, int32_t *launches) {
-    int rc = group_check(hs, n, nullptr);
+    int rc = group_check(hs, n, nullptr, false);   // a plan needs only the handles' configs
     if (rc) return rc;
     if (!launch_of || !launches) return fail(hs[0], MRTS_EINVAL, "step_group_plan: null output");
     EngineParams ps[MRTS_STEP_GROUP_MAX];
     int lo[MRTS_STEP_GROUP_MAX];
     for (int i = 0; i < n; i++) {
-        ps[i] = hs[i]->base;
+        ps[i] = EngineParams{};
+        ps[i].HW = hs[i]->HW;
+        ps[i].W = hs[i]->W;
+        ps[i].partial_obs = hs[i]->partial_obs;
+        ps[i].obs_float = hs[i]->obs_float;
         ps[i].fuse_bots = fused(hs[i]) ? 1 : 0;
     }
     *launches = group_plan(ps, n, policy, lo);

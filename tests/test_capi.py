@@ -131,3 +131,36 @@ def test_fused_early_bot_layout_is_race_free_for_every_size():
     odd = [(w, h) for w, h in fusable if (w * h) % 4]
     assert (15, 15) in odd and (9, 13) in odd and (3, 5) in odd
     assert f(8, 8) == 1 and f(4, 4) == 1 and f(33, 16) == -1 and f(0, 5) == -1
+
+
+def test_step_group_plan_merges_what_fits():
+    """mrts_step_group_plan (host logic, no workspace needed): configs[4]'s buckets -- 8x8 and
+    16x16 share a launch under merge-fit, 24x24 (52 KB fused workgroups) keeps its own;
+    merge-all puts all three in one; separate gives one each; engines of other planes or
+    bot fusion never share; a handle listed twice is rejected."""
+    from gym_microrts import _native
+
+    lib = _native.lib()
+
+    def mk(m, bots=2, partial=False):
+        return _create(map_paths=[os.path.join(MAPS, m)], game_map=[0] * (2 + bots), bot_ai=[4] * bots, num_bot_envs=bots,
+                       partial_obs=partial)
+
+    def plan(hs, policy):
+        arr = (ctypes.c_void_p * len(hs))(*hs)
+        lo, nl = (ctypes.c_int32 * len(hs))(), ctypes.c_int32()
+        rc = lib.mrts_step_group_plan(arr, len(hs), policy, lo, ctypes.byref(nl))
+        return rc, list(lo), nl.value
+
+    h8, h16, h24 = mk("maps/8x8/basesWorkers8x8.xml"), mk("maps/16x16/basesWorkers16x16.xml"), mk("maps/24x24/basesWorkers24x24.xml")
+    hs = [h8, h16, h24]
+    assert plan(hs, _native.GROUP_MERGE_FIT | _native.GROUP_BOTS_FIRST) == (0, [0, 0, 1], 2)
+    assert plan(hs, _native.GROUP_MERGE_ALL) == (0, [0, 0, 0], 1)
+    assert plan(hs, _native.GROUP_SEPARATE) == (0, [0, 1, 2], 3)
+    hp = mk("maps/10x10/basesTwoWorkers10x10.xml", partial=True)   # 31 planes: its own launch
+    hsp = mk("maps/4x4/baseTwoWorkers4x4.xml", bots=0)             # no bots: not fused, its own launch
+    assert plan([h16, hp, hsp], _native.GROUP_MERGE_ALL) == (0, [0, 1, 2], 3)
+    rc, _, _ = plan([h16, h16], _native.GROUP_MERGE_ALL)
+    assert rc != 0 and b"twice" in lib.mrts_last_error(h16)
+    for h in hs + [hp, hsp]:
+        lib.mrts_destroy(h)
