@@ -1594,6 +1594,7 @@ static hipError_t step_group(const EngineParams* ps, int n, hipStream_t s, bool 
         if (fused) e.early_bot = early_bot_disjoint(e.HW, e.W, NT) ? 1 : 0;   // the layout at this launch's NT
         sh = std::max(sh, fused ? fb_lds_bytes(e.HW, e.W, NT) : lds_bytes(e.HW, e.W, NT));
     }
+    if (sh > 163840) return hipErrorInvalidValue;   // one workgroup's LDS on a CU
     int grid = 0;
     auto seg = [&](int m, int g0, int g1) {
         if (g1 <= g0) return;
