@@ -508,8 +508,9 @@ static int group_plan(const EngineParams *ps, int n, int policy, int *launch_of)
     return nl;
 }
 
-static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io, bool need_bound = true) {
+static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io, int32_t policy, bool need_bound = true) {
     if (!hs || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(nullptr, MRTS_EINVAL, "step_group: bad arguments");
+    if ((policy & ~7) || (policy & 3) == 3) return fail(hs[0], MRTS_EINVAL, "step_group: unknown policy bits");
     for (int i = 0; i < n; i++) {
         if (!hs[i]) return fail(nullptr, MRTS_EINVAL, "step_group: null handle");
         if ((need_bound && !bound(hs[i])) || (io && !io_ok(io[i], io[i].reward != nullptr)))
@@ -521,7 +522,7 @@ static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io, b
 }
 
 int mrts_step_group_plan(mrts_vec *const *hs, int32_t n, int32_t policy, int32_t *launch_of, int32_t *launches) {
-    int rc = group_check(hs, n, nullptr, false);   // a plan needs only the handles' configs
+    int rc = group_check(hs, n, nullptr, policy, false);   // a plan needs only the handles' configs
     if (rc) return rc;
     if (!launch_of || !launches) return fail(hs[0], MRTS_EINVAL, "step_group_plan: null output");
     EngineParams ps[MRTS_STEP_GROUP_MAX];
@@ -540,7 +541,7 @@ int mrts_step_group_plan(mrts_vec *const *hs, int32_t n, int32_t policy, int32_t
 }
 
 int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy) {
-    int rc = group_check(hs, n, io);
+    int rc = group_check(hs, n, io, policy);
     if (rc) return rc;
     if (!io) return fail(hs[0], MRTS_EINVAL, "step_group: null io");
     hipStream_t s = (hipStream_t)stream;

@@ -162,5 +162,8 @@ def test_step_group_plan_merges_what_fits():
     assert plan([h16, hp, hsp], _native.GROUP_MERGE_ALL) == (0, [0, 1, 2], 3)
     rc, _, _ = plan([h16, h16], _native.GROUP_MERGE_ALL)
     assert rc != 0 and b"twice" in lib.mrts_last_error(h16)
+    for bad in (3, 8):
+        rc, _, _ = plan(hs, bad)
+        assert rc != 0 and b"policy" in lib.mrts_last_error(h8)
     for h in hs + [hp, hsp]:
         lib.mrts_destroy(h)
