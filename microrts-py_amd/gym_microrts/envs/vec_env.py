@@ -479,6 +479,10 @@ class MicroRTSGridModeVecEnv:
             obs = self._host("obs", self._obs)
             if prefetch:
                 self._mask_prefetch = self._host("mask", self._mask)
+        # vec_env.py:1036: one dict per env around a row VIEW of the raw rewards -- built
+        # while the copies above are in flight (views read nothing; they see the rows
+        # the copy lands and the shaping mask below, as the reference's do)
+        infos = [{"raw_rewards": item} for item in reward]
         self._sync()
         self._act_src = None
         done = done.astype(bool)
@@ -491,7 +495,6 @@ class MicroRTSGridModeVecEnv:
                 if prefetch:
                     self._mask_prefetch = self._host("mask", self._mask)
                 self._sync()
-        infos = [{"raw_rewards": item} for item in reward]
         return obs, reward @ self.reward_weight, done[:, 0], infos
 
     def _step_io(self):
