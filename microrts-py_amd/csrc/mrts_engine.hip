@@ -1504,11 +1504,24 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
 // launchers
 
 
+// One engine's step launch.  With both selfplay and bot games, the bot games take
+// the first workgroups: workgroups start in grid order, and a bot game's chain (the
+// fused bot after the tick) is the longest, so the short selfplay games fill the last
+// round (4096 selfplay + 4096 bot envs, 16x16: step 215 -> 196 us,
+// profiles/r03_ab/ab20_single_engine_bots_first/).
 static StepGroup one_engine(const EngineParams& p) {
     StepGroup sg{};
     sg.e[0] = p;
-    sg.seg_block[1] = p.G;
-    sg.nseg = 1;
+    if (p.nsp_games > 0 && p.nsp_games < p.G) {
+        sg.seg_game[0] = p.nsp_games;
+        sg.seg_block[1] = p.G - p.nsp_games;
+        sg.seg_game[1] = 0;
+        sg.seg_block[2] = p.G;
+        sg.nseg = 2;
+    } else {
+        sg.seg_block[1] = p.G;
+        sg.nseg = 1;
+    }
     return sg;
 }
 
