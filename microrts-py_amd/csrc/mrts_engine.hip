@@ -15,6 +15,8 @@
 // on lane 0 over compact ballot-built lists, which hold only the few units
 // that act this tick.  Outputs are written with 16-byte stores from compact
 // per-cell bit words in LDS (one-hot obs: 1 word/cell, mask: 3 words/cell).
+// A step launch takes a StepGroup: one or more engines (map-size buckets) cut
+// into grid segments, bot games first (mrts_step_group).
 //
 // Integer work only: no MFMA, the kernels are HBM-bound on the obs/mask writes.
 #include <hip/hip_runtime.h>
