@@ -164,7 +164,10 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
  * >= 4 workgroups per CU at the launch's LDS size; larger maps keep their own
  * launch), MRTS_GROUP_MERGE_ALL (every compatible member), | MRTS_GROUP_BOTS_FIRST
  * (bot games start before selfplay games in the merged grid).  Outputs are the
- * same bytes whatever the policy.  1 <= n <= MRTS_STEP_GROUP_MAX, each handle once. */
+ * same bytes whatever the policy.  1 <= n <= MRTS_STEP_GROUP_MAX, each handle once,
+ * all on the device that runs `stream`.  Errors: the message is on the failing
+ * member's handle and on hs[0].  Not atomic: when launch l fails with MRTS_EHIP the
+ * members of earlier launches have stepped and the others have not. */
 #define MRTS_STEP_GROUP_MAX 4
 #define MRTS_GROUP_SEPARATE 0
 #define MRTS_GROUP_MERGE_FIT 1
@@ -242,7 +245,7 @@ int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out);
  * handle): 1 = the bot may start beside the output words' build (its LDS writes
  * and that phase's reads / writes are disjoint, checked from both carves),
  * 0 = fusable but the bot waits for that phase, -1 = no bot fusion for this
- * size.  No reference counterpart (an engine-internal schedule). */
+ * size (fused LDS over 160 KB, or a bot LDS over the 64 KB mrts_create allows).  No reference counterpart (an engine-internal schedule). */
 int mrts_fused_layout_ok(int32_t width, int32_t height);
 
 /* UnitTypeTable JSON as rts.units.UnitTypeTable.toJSON / sendUTT()

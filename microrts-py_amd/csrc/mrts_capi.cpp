@@ -508,15 +508,25 @@ static int group_plan(const EngineParams *ps, int n, int policy, int *launch_of)
     return nl;
 }
 
+// A group call's error is recorded on the member it concerns AND on hs[0], the
+// handle callers read mrts_last_error from (a failure of member i > 0
+// used to leave hs[0]'s message empty or stale).
+static int group_fail(mrts_vec *const *hs, int i, int code, const std::string &msg) {
+    const std::string m = i > 0 ? msg + " (member " + std::to_string(i) + ")" : msg;
+    if (hs && i >= 0 && hs[i]) hs[i]->err = m;
+    if (hs && hs[0]) hs[0]->err = m;
+    return code;
+}
+
 static int group_check(mrts_vec *const *hs, int32_t n, const mrts_step_io *io, int32_t policy, bool need_bound = true) {
-    if (!hs || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(nullptr, MRTS_EINVAL, "step_group: bad arguments");
-    if ((policy & ~7) || (policy & 3) == 3) return fail(hs[0], MRTS_EINVAL, "step_group: unknown policy bits");
+    if (!hs || n < 1 || n > MRTS_STEP_GROUP_MAX) return fail(hs && n >= 1 ? hs[0] : nullptr, MRTS_EINVAL, "step_group: bad arguments");
+    if ((policy & ~7) || (policy & 3) == 3) return group_fail(hs, 0, MRTS_EINVAL, "step_group: unknown policy bits");
     for (int i = 0; i < n; i++) {
-        if (!hs[i]) return fail(nullptr, MRTS_EINVAL, "step_group: null handle");
+        if (!hs[i]) return group_fail(hs, i, MRTS_EINVAL, "step_group: null handle");
         if ((need_bound && !bound(hs[i])) || (io && !io_ok(io[i], io[i].reward != nullptr)))
-            return fail(hs[i], MRTS_ESTATE, "step_group: workspace not bound or null buffer");
+            return group_fail(hs, i, MRTS_ESTATE, "step_group: workspace not bound or null buffer");
         for (int j = 0; j < i; j++)
-            if (hs[j] == hs[i]) return fail(hs[i], MRTS_EINVAL, "step_group: an engine listed twice");
+            if (hs[j] == hs[i]) return group_fail(hs, i, MRTS_EINVAL, "step_group: an engine listed twice");
     }
     return MRTS_OK;
 }
@@ -543,7 +553,7 @@ int mrts_step_group_plan(mrts_vec *const *hs, int32_t n, int32_t policy, int32_t
 int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_step_io *io, int32_t policy) {
     int rc = group_check(hs, n, io, policy);
     if (rc) return rc;
-    if (!io) return fail(hs[0], MRTS_EINVAL, "step_group: null io");
+    if (!io) return group_fail(hs, 0, MRTS_EINVAL, "step_group: null io");
     hipStream_t s = (hipStream_t)stream;
     EngineParams ps[MRTS_STEP_GROUP_MAX];
     for (int i = 0; i < n; i++) {
@@ -551,7 +561,8 @@ int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_ste
         ps[i] = step_params(h, io[i]);
         // the tick's bot decisions, when an earlier launch did not make them
         hipError_t e = h->bots_ready ? hipSuccess : mrts_engine_bots(&ps[i], s);
-        if (e) return hip_fail(h, e, "step_group bot launch");
+        if (e) return group_fail(hs, i, MRTS_EHIP, std::string("step_group bot launch: ") + hipGetErrorString(e));
+        h->bots_ready = true;   // this tick's decisions are in botpa now, whatever happens below
         ps[i].fuse_bots = fused(h) ? 1 : 0;
     }
     int launch_of[MRTS_STEP_GROUP_MAX];
@@ -565,9 +576,12 @@ int mrts_step_group(mrts_vec *const *hs, int32_t n, void *stream, const mrts_ste
                 grp[m++] = ps[i];
             }
         hipError_t e = mrts_engine_step_group(grp, m, s, (policy & MRTS_GROUP_BOTS_FIRST) != 0);
-        if (e) return hip_fail(hs[first], e, "step_group launch");
+        // not atomic: members of launches 0..l-1 have stepped, those of l.. have not
+        // (include/microrts_amd.h); each member's bot state follows its own launch
+        if (e) return group_fail(hs, first, MRTS_EHIP, std::string("step_group launch: ") + hipGetErrorString(e));
+        for (int i = 0; i < n; i++)
+            if (launch_of[i] == l) hs[i]->bots_ready = ps[i].fuse_bots != 0;
     }
-    for (int i = 0; i < n; i++) hs[i]->bots_ready = ps[i].fuse_bots != 0;
     return MRTS_OK;
 }
 
@@ -731,6 +745,7 @@ int mrts_fused_layout_ok(int32_t width, int32_t height) {
     if (width <= 0 || height <= 0 || width > 32 || height > 64) return -1;
     const int HW = width * height;
     if (mrts_engine_fused_lds_bytes(HW, width) > 163840) return -1;
+    if (mrts_engine_bot_lds_bytes(HW, width) > 65536) return -1;   // mrts_create refuses such bot engines
     return mrts_engine_early_bot_ok(HW, width);
 }
 

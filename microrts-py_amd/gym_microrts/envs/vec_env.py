@@ -795,8 +795,10 @@ class MicroRTSMixedMapVecEnv:
         if group_policy == "default":
             group_policy = _native.GROUP_MERGE_FIT | _native.GROUP_BOTS_FIRST
         self.group_policy = group_policy
+        # (one launch runs on one device: buckets placed on different GPUs step one by one)
         self.grouped = (group_policy is not None and not self.concurrent and 1 < len(self.envs) <= _native.STEP_GROUP_MAX
-                        and all(e.contract == "tensors" and len(e.cycle_maps) <= e._cycle_min for e in self.envs))
+                        and all(e.contract == "tensors" and len(e.cycle_maps) <= e._cycle_min for e in self.envs)
+                        and all(e.device == self.envs[0].device for e in self.envs))
 
     def launch_plan(self):
         """(launch index of each bucket, launches per step) of the grouped step

@@ -65,8 +65,12 @@ def main(argv=None):
     if argv[0].startswith("--contract"):
         if "=" in argv[0]:
             contract, argv = argv[0].split("=", 1)[1], argv[1:]
-        else:
+        elif len(argv) >= 2:
             contract, argv = argv[1], argv[2:]
+        else:
+            print("--contract needs a value: numpy | tensors | hybrid", file=sys.stderr)
+            print(__doc__)
+            return 2
         if contract not in ("numpy", "tensors", "hybrid"):
             print(f"unknown contract {contract!r}: numpy | tensors | hybrid", file=sys.stderr)
             return 2

@@ -7,7 +7,7 @@ L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
 for round in $(seq 1 $3); do
   for v in $2; do
-    cp exp_libs/lib$v.so $L
+    cp scripts/ab/lib$v.so $L
     line="$v $round"
     for n in 512 2048 8192; do
       timeout -k 10 200 python bench.py --no-cpu-baseline --steps 150 --envs-per-gpu $n > $O/head_${v}_$n.$round.json 2>/dev/null

@@ -7,7 +7,7 @@ L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
 for round in $(seq 1 $3); do
   for v in $2; do
-    cp exp_libs/lib$v.so $L
+    cp scripts/ab/lib$v.so $L
     line="$v $round"
     for wl in $4; do
       w=${wl%%:*}; n=${wl##*:}

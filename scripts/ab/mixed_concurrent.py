@@ -3,13 +3,13 @@ streams -- the merged 8x8 + 16x16 launch on one, the 24x24 launch on another, fo
 and joined back into the caller's stream -- vs the product's back-to-back launches.
 Runs bench.py's mixed workload with MicroRTSMixedMapVecEnv.step_wait patched.
 
-  python exp_libs/mixed_concurrent.py [bench args...]
+  python scripts/ab/mixed_concurrent.py [bench args...]
 """
 import ctypes
 import os
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "microrts-py_amd"))
 import torch  # noqa: E402

@@ -5,7 +5,7 @@ import sys
 
 import numpy as np  # noqa: F401
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "microrts-py_amd"))
 from gym_microrts import _native  # noqa: E402,F401

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/$1; mkdir -p $O
 L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
-cp exp_libs/libord.so $L
+cp scripts/ab/libord.so $L
 for m in 1 2 3; do
   MRTS_EXP_ORDER=$m timeout -k 10 300 python -m pytest tests/test_gpu_bots.py -m gpu -q -k "mixed_map_buckets and False-5" > $O/parity_$m.txt 2>&1 && echo "parity ok $m" || { echo "PARITY FAIL $m"; tail -5 $O/parity_$m.txt; cp /tmp/lib_product.so $L; exit 1; }
 done

@@ -6,11 +6,11 @@ O=gpurun_out/$1; mkdir -p $O
 L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
 for v in $2; do
-  cp exp_libs/lib$v.so $L
-  if ! timeout -k 10 400 python exp_libs/quick_parity.py > $O/parity_$v.txt 2>&1; then
+  cp scripts/ab/lib$v.so $L
+  if ! timeout -k 10 400 python scripts/ab/quick_parity.py > $O/parity_$v.txt 2>&1; then
     echo "PARITY FAIL $v"; tail -5 $O/parity_$v.txt; cp /tmp/lib_product.so $L; exit 1
   fi
   echo "parity ok $v"
 done
 cp /tmp/lib_product.so $L
-bash exp_libs/ab.sh $1 "$3" ${4:-2}
+bash scripts/ab/ab.sh $1 "$3" ${4:-2}

@@ -11,19 +11,19 @@ O=gpurun_out/${1:-occ}; mkdir -p $O
 L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
 for v in s94 w8; do
-  cp exp_libs/lib$v.so $L
-  timeout -k 10 400 python exp_libs/quick_parity.py > $O/parity_$v.log 2>&1 && echo "parity ok $v" || { echo "parity FAILED $v"; tail -5 $O/parity_$v.log; }
+  cp scripts/ab/lib$v.so $L
+  timeout -k 10 400 python scripts/ab/quick_parity.py > $O/parity_$v.log 2>&1 && echo "parity ok $v" || { echo "parity FAILED $v"; tail -5 $O/parity_$v.log; }
 done
 for round in 1 2 3; do
   for v in base s94 w8; do
-    cp exp_libs/lib$v.so $L
+    cp scripts/ab/lib$v.so $L
     timeout -k 10 200 python bench.py --no-cpu-baseline --steps 150 > $O/head_$v.$round.json 2>/dev/null
     echo "$v $round head $(python -c "import json; d=json.load(open('$O/head_$v.$round.json')); print(d['value'], round(d['kernels']['step']['avg_ms']*1000,1), round(d['kernels']['sample']['avg_ms']*1000,1))")"
   done
 done
 B="bench.py --steps 40 --warmup 10 --no-cpu-baseline --no-kernel-events"
 for v in base s94 w8; do
-  cp exp_libs/lib$v.so $L
+  cp scripts/ab/lib$v.so $L
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -f csv -d "$O/sq_$v/a" -o a -- python3 $B > /dev/null 2> "$O/sq_$v.a.err"
   timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SALU -f csv -d "$O/sq_$v/b" -o b -- python3 $B > /dev/null 2> "$O/sq_$v.b.err"
   python3 scripts/sq_summary.py "$O/sq_$v" "$O/sq_$v.json" "$B ($v)"

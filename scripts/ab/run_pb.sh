@@ -11,13 +11,13 @@ cp $L /tmp/lib_product.so
 restore() { cp /tmp/lib_product.so $L; }
 trap restore EXIT
 for v in ${CANDS:-pb2 cs2}; do
-  cp exp_libs/lib$v.so $L
-  timeout -k 10 400 python exp_libs/quick_parity.py > $O/parity_$v.log 2>&1 || { echo "parity FAILED $v"; tail -8 $O/parity_$v.log; exit 1; }
+  cp scripts/ab/lib$v.so $L
+  timeout -k 10 400 python scripts/ab/quick_parity.py > $O/parity_$v.log 2>&1 || { echo "parity FAILED $v"; tail -8 $O/parity_$v.log; exit 1; }
   echo "parity ok $v"
 done
 for round in 1 2 3; do
   for v in new ${CANDS:-pb2 cs2}; do
-    cp exp_libs/lib$v.so $L
+    cp scripts/ab/lib$v.so $L
     timeout -k 10 200 python bench.py --no-cpu-baseline --steps 150 > $O/head_$v.$round.json 2>/dev/null
     timeout -k 10 200 python bench.py --no-cpu-baseline --workload coac --envs-per-gpu 1024 --steps 300 > $O/coac_$v.$round.json 2>/dev/null
     echo "$v $round head $(python -c "import json; d=json.load(open('$O/head_$v.$round.json')); print(d['value'], round(d['kernels']['step']['avg_ms']*1000,1), round(d['kernels']['sample']['avg_ms']*1000,1))") coac $(python -c "import json; d=json.load(open('$O/coac_$v.$round.json')); print(d['value'], round(d['kernels']['step']['avg_ms']*1000,1), round(d['kernels']['sample']['avg_ms']*1000,1))")"

@@ -11,15 +11,15 @@ L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
 restore() { cp /tmp/lib_product.so $L; }
 trap restore EXIT
-cp exp_libs/libbar.so $L
+cp scripts/ab/libbar.so $L
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shard.py -k sampler -x -v --timeout 200 --timeout-method thread > $O/pytest_sampler.log 2>&1 \
   || { echo "pytest failed"; tail -30 $O/pytest_sampler.log; exit 1; }
 tail -1 $O/pytest_sampler.log
-timeout -k 10 400 python exp_libs/quick_parity.py > $O/parity_bar.log 2>&1 || { echo "parity FAILED bar"; tail -8 $O/parity_bar.log; exit 1; }
+timeout -k 10 400 python scripts/ab/quick_parity.py > $O/parity_bar.log 2>&1 || { echo "parity FAILED bar"; tail -8 $O/parity_bar.log; exit 1; }
 echo "parity ok bar"
 for round in 1 2 3; do
   for v in base phx bar; do
-    cp exp_libs/lib$v.so $L
+    cp scripts/ab/lib$v.so $L
     timeout -k 10 200 python bench.py --no-cpu-baseline --steps 150 > $O/head_$v.$round.json 2>/dev/null
     timeout -k 10 200 python bench.py --no-cpu-baseline --workload coac --envs-per-gpu 1024 --steps 300 > $O/coac_$v.$round.json 2>/dev/null
     echo "$v $round head $(python -c "import json; d=json.load(open('$O/head_$v.$round.json')); print(d['value'], round(d['kernels']['step']['avg_ms']*1000,1), round(d['kernels']['sample']['avg_ms']*1000,1))") coac $(python -c "import json; d=json.load(open('$O/coac_$v.$round.json')); print(d['value'], round(d['kernels']['step']['avg_ms']*1000,1), round(d['kernels']['sample']['avg_ms']*1000,1))")"

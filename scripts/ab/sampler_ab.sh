@@ -7,16 +7,16 @@ O=gpurun_out/$1; mkdir -p $O
 L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
 for v in $2; do
-  cp exp_libs/lib$v.so $L
+  cp scripts/ab/lib$v.so $L
   if ! timeout -k 10 300 python -m pytest tests/test_gpu_parity.py tests/test_gpu_shard.py -m gpu -q -k "sampler" > $O/parity_$v.txt 2>&1; then
     echo "PARITY FAIL $v"; tail -15 $O/parity_$v.txt; cp /tmp/lib_product.so $L; exit 1
   fi
-  case $v in *i) timeout -k 10 400 python exp_libs/quick_parity.py > $O/qparity_$v.txt 2>&1 || { echo "ENGINE PARITY FAIL $v"; tail -5 $O/qparity_$v.txt; cp /tmp/lib_product.so $L; exit 1; };; esac
+  case $v in *i) timeout -k 10 400 python scripts/ab/quick_parity.py > $O/qparity_$v.txt 2>&1 || { echo "ENGINE PARITY FAIL $v"; tail -5 $O/qparity_$v.txt; cp /tmp/lib_product.so $L; exit 1; };; esac
   echo "parity ok $v: $(tail -1 $O/parity_$v.txt)"
 done
 for round in $(seq 1 ${3:-2}); do
   for v in $2; do
-    cp exp_libs/lib$v.so $L
+    cp scripts/ab/lib$v.so $L
     timeout -k 10 200 python bench.py --no-cpu-baseline --steps 150 > $O/head_$v.$round.json 2>/dev/null
     timeout -k 10 200 python bench.py --workload coac --envs-per-gpu 1024 --no-cpu-baseline --steps 300 > $O/coac_$v.$round.json 2>/dev/null
     python - $O/head_$v.$round.json $O/coac_$v.$round.json $v $round <<'PY'

@@ -3,7 +3,7 @@ overlapped copies (three blocking copies, infos after them) -- same-box A/B base
 import os
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "microrts-py_amd"))
 from gym_microrts.envs import vec_env  # noqa: E402

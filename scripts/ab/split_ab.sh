@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/$1; mkdir -p $O
 L=microrts-py_amd/gym_microrts/libmicrorts_amd.so
 cp $L /tmp/lib_product.so
-cp exp_libs/libsplit.so $L
+cp scripts/ab/libsplit.so $L
 MRTS_EXP_SPLIT=512 timeout -k 10 300 python -m pytest tests/test_gpu_fullsize.py -m gpu -q -k "selfplay_8192" > $O/parity.txt 2>&1 && echo "parity ok" || { echo "parity FAIL"; tail -5 $O/parity.txt; }
 for round in 1 2; do
   for K in 0 256 512 1024 1536; do

@@ -241,3 +241,4 @@ def test_run_driver_contract_flag(tmp_path, monkeypatch):
     assert run_driver.main(["--contract=tensors", str(script)]) == 0
     assert out.read_text() == "tensors"
     assert run_driver.main(["--contract", "nope", str(script)]) == 2
+    assert run_driver.main(["--contract"]) == 2   # no value: usage, not IndexError
