@@ -7,15 +7,21 @@ per-step API traffic of the reference rollout loop.  Workload:
 max_steps 2000, auto-reset on, inputs already resident in HBM.
 
   python bench.py [--gpus N --steps K --warmup W]
-  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N>1: either under a launcher (python -m torch.distributed.run --nproc-per-node N
+       ... bench.py --gpus N: WORLD_SIZE must equal N), or plain `bench.py --gpus N`,
+       which starts the N ranks itself as child processes (launch_ranks) before
+       anything in the parent touches torch or HIP, relays rank 0's line and exits
+       with the worst child status.
 Each rank owns an independent contiguous shard of envs (no data-path
 collective: envs never interact); the only communication is the timing
 barrier and the max-over-ranks of the elapsed time.
 
-Rank 0 prints one JSON line.  `roofline` prices the dominant kernel with HIP
-events recorded around its launches on every 8th step of the timed region;
-`cpu_baseline` times the CPU restatement (oracle/, OpenMP over games) on a
-bounded sample of the same workload (rank 0, N=1 only).
+Rank 0 prints one JSON line.  The timed region carries no HIP events;
+`roofline` prices the dominant kernel from a separate pass of --roofline-steps
+(>= 64) steps right after it, with HIP events around every launch of every step
+(`roofline.samples` launches); `cpu_baseline` times the CPU restatement
+(oracle/, OpenMP over games) on a bounded sample of the same workload (rank 0,
+N=1 only).
 """
 import argparse
 import json
@@ -31,7 +37,7 @@ MAP = "maps/16x16/basesWorkers16x16.xml"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
@@ -44,9 +50,10 @@ def parse():
                          "each); the line reports the median run (BASELINE.md §3: median of 3 seeds) and every seed's value")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-events", action="store_true")
-    ap.add_argument("--event-every", type=int, default=8,
-                    help="record per-launch HIP events on every N-th step of the timed region")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="skip the event-timed roofline pass (no roofline / kernels in the line)")
+    ap.add_argument("--roofline-steps", type=int, default=64,
+                    help="steps of the event-timed pass after the timed window (HIP events around every launch)")
     ap.add_argument("--bot-fusion", type=int, default=1, choices=[0, 1],
                     help="mrts_set_bot_fusion: 0 k_bot at every step, 1 k_step decides the next tick's bot actions")
     ap.add_argument("--api", default="tensor", choices=["tensor", "numpy", "sharedmem"],
@@ -74,7 +81,7 @@ def parse():
                          "or 'none' = one step launch per bucket")
     ap.add_argument("--dump", default=None,
                     help="save each rank's final obs / masks / raw rewards / dones to DUMP.rank<r>.npz (shard tests)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # BASELINE.json configs as bench workloads: (map, selfplay envs, bot envs, bot, partial_obs).
@@ -138,7 +145,22 @@ def window_stats(before, after, steps):
             "ordered_issue_rows_per_step": round(float((a[:, 4] - b[:, 4]).sum()) / steps, 1)}
 
 
-def run_mixed(args, rank, dev):
+def roofline_pass(args, one_step, timing, s1):
+    """The event-timed pass priced by `roofline`: --roofline-steps more steps of the
+    same loop right after the timed window (which itself records no events), with
+    HIP events around every launch of every step."""
+    import torch
+
+    if args.no_kernel_events or args.roofline_steps <= 0:
+        return
+    timing[0] = True
+    for s in range(s1, s1 + args.roofline_steps):
+        one_step(s)
+    torch.cuda.synchronize()
+    timing[0] = False
+
+
+def run_mixed(args, rank, world, dev):
     """BASELINE configs[4]: one MicroRTSMixedMapVecEnv with an 8x8, a 16x16 and a 24x24
     bucket, each half selfplay envs, a quarter vs device workerRushAI, a quarter vs
     device coacAI; envs_per_gpu split 1:2:1 over the buckets."""
@@ -167,7 +189,7 @@ def run_mixed(args, rank, dev):
 
     def one_step(s):
         masks = env.get_action_mask()
-        rec = timing[0] and s % args.event_every == 0
+        rec = timing[0]
         for e, m, a in zip(env.envs, masks, acts):
             e.kernel_events = ev.setdefault(e.height, {}) if rec else None
             _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, rank * e.num_envs,
@@ -183,21 +205,23 @@ def run_mixed(args, rank, dev):
         return out
 
     env.reset()
-    s0 = preroll(env.envs, one_step, args.max_steps if args.preroll < 0 else args.preroll, rank,
-                 int(os.environ.get("WORLD_SIZE", "1")))
+    s0 = preroll(env.envs, one_step, args.max_steps if args.preroll < 0 else args.preroll, rank, world)
     for s in range(s0, s0 + args.warmup):
         one_step(s)
     torch.cuda.synchronize()
     before = [e.game_stats() for e in env.envs]
-    timing[0] = not args.no_kernel_events
+    barrier(world, dev)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(s0 + args.warmup, s0 + args.warmup + args.steps):
         one_step(s)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    barrier(world, dev)
+    after = [e.game_stats() for e in env.envs]
+    roofline_pass(args, one_step, timing, s0 + args.warmup + args.steps)
     for e in env.envs:
         e.kernel_events = None
-    after = [e.game_stats() for e in env.envs]
     # per bucket: mean step-kernel launch time and its algorithmic bytes
     buckets = []
     for e in env.envs:
@@ -208,6 +232,7 @@ def run_mixed(args, rank, dev):
                         "step_bytes": kb["step"]})
     stats = window_stats(before, after, args.steps)
     stats["buckets"] = buckets
+    stats["roofline_samples"] = len(ev.get("all", []))
     stats["buckets_concurrent"] = env.concurrent
     stats["group_policy"] = env.group_policy if env.grouped else None
     stats["bucket_launch"], stats["launches_per_step"] = env.launch_plan()
@@ -343,10 +368,10 @@ def run_gpu(args, rank, world, local_rank):
     ev = {}
 
     def one_step(s):
-        # HIP events around every launch of every `event_every`-th step of the
-        # timed region (each event is a queue packet between dependent kernels;
-        # recording all of them costs ~7 % of the step)
-        env.kernel_events = ev if (timing[0] and s % args.event_every == 0) else None
+        # HIP events around every launch, in the roofline pass only (each event is a
+        # queue packet between dependent kernels: ~7 % of the step, kept out of the
+        # timed window)
+        env.kernel_events = ev if timing[0] else None
         m = env.get_action_mask()   # numpy api: the (N, HW, 78) host copy ppo_gridnet.py:466 makes
         if env.kernel_events is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -372,7 +397,6 @@ def run_gpu(args, rank, world, local_rank):
         one_step(s)
     torch.cuda.synchronize()
     before = [env.game_stats()]
-    timing[0] = not args.no_kernel_events
     barrier(world, dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -382,13 +406,15 @@ def run_gpu(args, rank, world, local_rank):
     t1 = time.perf_counter()
     barrier(world, dev)
     elapsed = t1 - t0
-    env.kernel_events = None
     stats = window_stats(before, [env.game_stats()], args.steps)
     stats["preroll_ticks"] = s0
     if args.dump:
         np.savez(f"{args.dump}.rank{rank}.npz", obs=obs.cpu().numpy(), mask=env._mask.cpu().numpy(),
                  src=env._src.cpu().numpy(), raw=env._raw.cpu().numpy(), done=env._done.cpu().numpy(),
                  stats=env.game_stats(), env0=env0)
+    roofline_pass(args, one_step, timing, s0 + args.warmup + args.steps)
+    env.kernel_events = None
+    stats["roofline_samples"] = len(ev.get("step", []))
     flags = env.error_flags()
     kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}  # ms per launch
     G = nsp // 2 + nbot
@@ -498,22 +524,81 @@ def cpu_sample(seconds, envs=512, workload="selfplay"):
                       f"encode in C, OpenMP over envs, OMP_NUM_THREADS={threads}"}
 
 
-def main():
-    if len(sys.argv) == 4 and sys.argv[1] == "--cpu-sample":   # child of cpu_baseline (no GPU use)
-        print(json.dumps(cpu_sample(float(sys.argv[2]), envs=64, workload=sys.argv[3])), flush=True)
-        return
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def _free_port():
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, popen=None, poll_s=0.2):
+    """`bench.py --gpus N` without a launcher: start ranks 0..N-1 of this same
+    command as fresh child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    in their environment, as torch.distributed.run sets them), relay their output,
+    and return the worst exit status.  Runs before the parent imports torch, so the
+    parent never initialises HIP (children start from a clean process; no exec).
+    When a rank fails, the others are terminated (they would wait in the barrier)."""
+    import subprocess
+
+    popen = popen or subprocess.Popen
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, MICRORTS_BENCH_SELF_LAUNCHED="1")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [None] * n
+    cause = 0   # the status of the first rank seen failing (the others are then stopped)
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0) and not cause:
+                    cause = rcs[r]
+        if cause:
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    try:
+                        rcs[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[r] = p.wait()
+            break
+        time.sleep(poll_s)
+    if cause:
+        print(f"bench.py: rank exit statuses {rcs}", file=sys.stderr)
+        return cause if cause > 0 else 128 - cause   # killed by signal k: 128 + k, as a shell reports it
+    return 0
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if len(argv) == 3 and argv[0] == "--cpu-sample":   # child of cpu_baseline (no GPU use)
+        print(json.dumps(cpu_sample(float(argv[1]), envs=64, workload=argv[2])), flush=True)
+        return 0
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return launch_ranks(args.gpus, argv)
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+            return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
     # one GPU per rank; ranks beyond the visible GPUs share them (gloo shard tests on a 1-GPU box)
-    local_rank %= max(1, torch.cuda.device_count())
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    import torch
-
+    ndev = max(1, torch.cuda.device_count())
+    local_rank %= ndev
+    pg = None
     if world > 1:
         import torch.distributed as dist
 
@@ -522,9 +607,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group("gloo")
+        pg = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "visible_devices": ndev,
+              "launcher": "bench.py (self-launched ranks)" if os.environ.get("MICRORTS_BENCH_SELF_LAUNCHED")
+              else "external (torch.distributed.run or equivalent)"}
     if args.workload == "mixed":
         torch.cuda.set_device(local_rank)
-        elapsed, kern, flags, hw, G, N, P, src_rows, stats = run_mixed(args, rank, torch.device("cuda", local_rank))
+        elapsed, kern, flags, hw, G, N, P, src_rows, stats = run_mixed(args, rank, world, torch.device("cuda", local_rank))
     else:
         runs = []
         for i in range(max(1, args.seeds)):
@@ -567,7 +655,10 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else round(traffic / (kern[dom] * 1e-3) / 1e9, 1),
                     "traffic_bytes_per_launch": traffic, "traffic_source": tsrc,
-                    "algorithmic_bytes_per_launch": kb[dom], "kernel": dom, "avg_launch_ms": round(kern[dom], 4)}
+                    "algorithmic_bytes_per_launch": kb[dom], "kernel": dom, "avg_launch_ms": round(kern[dom], 4),
+                    "samples": stats.get("roofline_samples"),
+                    "timing": f"HIP events around every launch of a separate {args.roofline_steps}-step pass after the "
+                              "timed window (the timed window records none)"}
         bk = stats.get("buckets")
         if bk and (stats.get("step_all_buckets_ms") or all(b["step_ms"] for b in bk)):
             # configs[4]: one step kernel per size bucket -- the algorithmic bytes of all
@@ -587,7 +678,10 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else round(traffic / (tms * 1e-3) / 1e9, 1),
                     "traffic_bytes_per_step": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": tb,
-                    "kernel": "step (all size buckets)", "launches": nl, "avg_launch_ms": round(tms, 4)}
+                    "kernel": "step (all size buckets)", "launches": nl, "avg_launch_ms": round(tms, 4),
+                    "samples": stats.get("roofline_samples"),
+                    "timing": f"HIP events around every step call of a separate {args.roofline_steps}-step pass after "
+                              "the timed window (the timed window records none)"}
         wc = stats.get("box_write_ceiling")
         if roof and wc and roof.get("kernel") == "step":
             roof["frac_of_box_write_ceiling"] = round(roof["achieved"] / wc["GBps"], 4)
@@ -597,6 +691,7 @@ def main():
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
+            "process_group": pg,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed_max / args.steps, 4),
@@ -631,7 +726,8 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

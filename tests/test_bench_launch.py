@@ -1,0 +1,102 @@
+"""bench.py --gpus N starts its own N ranks when no launcher did.
+
+The parent must not initialise HIP before the children start (a process that
+touched the GPU must not fork/exec the ranks' runtime state, and the children
+each pick their own device): these tests run bench.main with `torch` replaced
+by a module that raises on any attribute access, and with subprocess.Popen
+replaced by a recorder, so they need no GPU.  The GPU end-to-end check (the
+self-launched ranks' dumps are the halves of a 1-rank run) is
+tests/test_gpu_shard.py::test_bench_self_launch_end_to_end.
+"""
+import os
+import subprocess
+import sys
+import types
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+class _NoTorch(types.ModuleType):
+    def __getattr__(self, name):
+        raise AssertionError(f"the launching parent touched torch.{name}")
+
+
+class _FakeProc:
+    def __init__(self, rc):
+        self.rc, self.terminated = rc, False
+
+    def poll(self):
+        return self.rc
+
+    def terminate(self):
+        self.terminated = True
+        self.rc = -15
+
+    def wait(self, timeout=None):
+        return self.rc
+
+    def kill(self):
+        self.rc = -9
+
+
+@pytest.fixture
+def no_torch(monkeypatch):
+    monkeypatch.setitem(sys.modules, "torch", _NoTorch("torch"))
+    monkeypatch.setitem(sys.modules, "torch.cuda", _NoTorch("torch.cuda"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MICRORTS_BENCH_SELF_LAUNCHED"):
+        monkeypatch.delenv(k, raising=False)
+
+
+def _recorder(monkeypatch, rcs):
+    calls = []
+
+    def popen(cmd, env=None, **kw):
+        calls.append((cmd, env))
+        return _FakeProc(rcs[len(calls) - 1])
+
+    monkeypatch.setattr(subprocess, "Popen", popen)
+    return calls
+
+
+def test_self_launch_starts_n_ranks_without_touching_torch(no_torch, monkeypatch):
+    calls = _recorder(monkeypatch, [0] * 8)
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    assert bench.main(argv) == 0
+    assert len(calls) == 8
+    ports = set()
+    for r, (cmd, env) in enumerate(calls):
+        assert cmd[0] == sys.executable and cmd[1].endswith("bench.py") and cmd[2:] == argv
+        assert env["RANK"] == env["LOCAL_RANK"] == str(r) and env["WORLD_SIZE"] == "8"
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+        ports.add(env["MASTER_PORT"])
+    assert len(ports) == 1   # one rendezvous
+
+
+def test_self_launch_failed_rank_stops_the_others(no_torch, monkeypatch):
+    procs = []
+
+    def popen(cmd, env=None, **kw):
+        p = _FakeProc(3 if env["RANK"] == "1" else None)
+        procs.append(p)
+        return p
+
+    monkeypatch.setattr(subprocess, "Popen", popen)
+    assert bench.main(["--gpus", "4"]) == 3
+    assert [p.terminated for p in procs] == [True, False, True, True]
+
+
+def test_world_size_must_match_gpus(no_torch, monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    assert bench.main(["--gpus", "4"]) == 2   # an error, before torch is imported
+
+
+def test_one_gpu_does_not_spawn(monkeypatch):
+    """--gpus 1 with no launcher runs in process (no child): the parse step only."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    args = bench.parse(["--gpus", "1", "--roofline-steps", "64"])
+    assert args.gpus == 1 and args.roofline_steps == 64 and not args.no_kernel_events

@@ -6,8 +6,9 @@ the random bots' streams the global game index, so each shard plays exactly its
 slice of one unsharded run.
 
 * in process: two shard engines of n envs == one engine of 2n envs, every step;
-* end to end: bench.py's own sharding path under torch.distributed.run with 2
-  ranks (gloo: both share the box's one GPU) == one bench.py process of 2n envs.
+* end to end: bench.py's own sharding path with 2 ranks (gloo: both share the
+  box's one GPU), under torch.distributed.run and self-launched by a plain
+  `bench.py --gpus 2`, == one bench.py process of 2n envs.
 """
 import os
 import socket
@@ -102,26 +103,48 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_bench_sharding_end_to_end(tmp_path):
-    """bench.py --gpus 2 over torch.distributed.run (2 ranks, gloo) dumps each rank's
-    final outputs; they are the two halves of a 1-rank bench.py run of twice the
-    envs (same seed, staggered pre-roll, warmup and timed steps)."""
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_bench_sharding_end_to_end(tmp_path, launcher):
+    """bench.py --gpus 2 (2 ranks, gloo) dumps each rank's final outputs; they are the
+    two halves of a 1-rank bench.py run of twice the envs (same seed, staggered
+    pre-roll, warmup and timed steps).  launcher = torchrun: under
+    torch.distributed.run; self: a plain `bench.py --gpus 2`, which starts its two
+    ranks itself (bench.launch_ranks) -- the driver's SCALE invocation."""
     common = ["--steps", "25", "--warmup", "3", "--preroll", "120", "--max-steps", "120", "--no-cpu-baseline",
-              "--no-kernel-events"]
+              "--roofline-steps", "8"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-                          "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
-                          "--envs-per-gpu", "256", "--dist-backend", "gloo", "--dump", str(tmp_path / "two")] + common,
-                         env=env, capture_output=True, text=True, timeout=240)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    bench = os.path.join(REPO, "bench.py")
+    two_args = ["--gpus", "2", "--envs-per-gpu", "256", "--dist-backend", "gloo", "--dump", str(tmp_path / "two")] + common
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+               "127.0.0.1", "--master-port", str(_free_port()), bench] + two_args
+    else:
+        cmd = [sys.executable, bench] + two_args
+    two = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert two.returncode == 0, two.stderr[-3000:]
-    one = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--envs-per-gpu", "512", "--dump", str(tmp_path / "one")]
+    one = subprocess.run([sys.executable, bench, "--envs-per-gpu", "512", "--dump", str(tmp_path / "one")]
                          + common, env=env, capture_output=True, text=True, timeout=240)
     assert one.returncode == 0, one.stderr[-3000:]
     import json
 
-    line = json.loads(two.stdout.strip().splitlines()[-1])
+    lines = [ln for ln in two.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, two.stdout[-3000:]   # rank 0 only
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["window"]["auto_resets"] > 0
+    assert line["process_group"]["world_size"] == 2 and line["process_group"]["backend"] == "gloo"
+    assert ("self" in line["process_group"]["launcher"]) == (launcher == "self")
+    assert line["roofline"]["samples"] == 8
     whole = np.load(tmp_path / "one.rank0.npz")
     parts = [np.load(tmp_path / f"two.rank{r}.npz") for r in range(2)]
     for k in ("obs", "mask", "src", "raw", "done", "stats"):
         np.testing.assert_array_equal(whole[k], np.concatenate([p[k] for p in parts]), err_msg=k)
+
+
+def test_bench_world_size_mismatch_fails():
+    """A launcher that started a different number of ranks than --gpus is an error."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
