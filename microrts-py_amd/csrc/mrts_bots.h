@@ -1280,14 +1280,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     for (int c = lane; S.partial && c < HW; c += BT) {
         const uint32_t u = L.unit[c];
         if (u == 0 || u_owner(u) != S.player) continue;
-        const int r = ut_sight(u_type(u)), x = c % W, y = c / W;
-        for (int dy = -r; dy <= r; dy++)
-            for (int dx = -r; dx <= r; dx++) {
-                const int xx = x + dx, yy = y + dy;
-                if (xx < 0 || yy < 0 || xx >= W || yy >= p.H || dx * dx + dy * dy > r * r) continue;
-                const int cc = yy * W + xx;
-                atomicOr(&L.vis[cc >> 5], 1u << (cc & 31));
-            }
+        or_sight_disk(L.vis, c % W, c / W, ut_sight(u_type(u)), W, p.H);
     }
     bot_sync<FUSED>();
     if (S.partial) {   // hide the units the player cannot observe
@@ -1375,6 +1368,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     // the closest enemy (list index) of each of the player's units, the scan
     // closest_enemy_index would do, all units at once (the state is fixed during
     // getAction): in lane k's kenemy, or L.pa[k] past 64 units; -1 = none
+    if (FUSED) MRTS_STAMP(10, lane == 0);
     const bool table = S.ai != MRTS_AI_RANDOM_BIASED && S.ai != MRTS_AI_RANDOM;
     S.kenemy = -1;
     if (table && n <= BT) {   // over the opponent's units only (scalar lane reads of their cells)
@@ -1424,6 +1418,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         if (S.n <= BT && S.naa <= BT) behaviours_parallel(S, L, coac ? 0 : army, po, coac);
         else if (coac) coac_serial(S, L);
         else rush_serial(S, L, army, po);
+        if (FUSED) MRTS_STAMP(11, lane == 0);
         translate_actions(S, L);
     } else if (S.ai == MRTS_AI_RANDOM_BIASED) {
         random_biased_get_action(S, L);
@@ -1431,6 +1426,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         random_single_get_action(S, L);
     }
     bot_sync<FUSED>();
+    if (FUSED) MRTS_STAMP(12, lane == 0);
     for (int i = lane; i < S.npa; i += BT) pa_g[i] = L.pa[i];
     for (int i = lane; i < 2 * S.naa; i += BT) aa_g[i] = L.aa[i];
     if (lane0()) {

@@ -5,6 +5,25 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Phase stamps (tracing, experiment builds only: `make STAMPS=1`): each step
+// workgroup takes a row of g_stamp and writes wall_clock64() (100 MHz) at its
+// phase boundaries; mrts_debug_stamps (mrts_engine.hip) reads the rows back.
+// Compiled out of the product library.
+#ifdef MRTS_STAMPS
+#define MRTS_STAMP_ROWS 65536
+#define MRTS_STAMP_COLS 16
+static __device__ unsigned long long g_stamp[MRTS_STAMP_ROWS][MRTS_STAMP_COLS];
+static __device__ unsigned int g_stamp_n;
+__shared__ int mrts_stamp_row;
+#define MRTS_STAMP(k, cond) \
+    do { if ((cond) && mrts_stamp_row < MRTS_STAMP_ROWS) g_stamp[mrts_stamp_row][k] = wall_clock64(); } while (0)
+#define MRTS_STAMP_MAX(k, cond) \
+    do { if ((cond) && mrts_stamp_row < MRTS_STAMP_ROWS) atomicMax(&g_stamp[mrts_stamp_row][k], (unsigned long long)wall_clock64()); } while (0)
+#else
+#define MRTS_STAMP(k, cond) do { } while (0)
+#define MRTS_STAMP_MAX(k, cond) do { } while (0)
+#endif
+
 struct EngineParams {
     int4 *cells;            // [G][HW]
     int32_t *genv;          // [G][MRTS_GENV_WORDS]

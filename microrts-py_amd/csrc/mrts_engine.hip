@@ -330,7 +330,8 @@ __device__ __forceinline__ void store_game(const EngineParams& p, const Lds& L, 
 // write the one-hot observation of one view: bits in L.aux, 16-byte stores
 // PartiallyObservableGameState.observable for both players: a cell is seen by
 // player q when some unit of q is within its sight radius (d^2 <= r^2).  Each
-// unit lane ORs its sight disk into the player's LDS bitmap.
+// unit lane ORs its sight disk into the player's LDS bitmap, one row span per
+// atomic (or_sight_disk).
 template <int NT>
 __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L) {
     const int HW = p.HW, nw = HW / 32 + 1;
@@ -340,18 +341,7 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
         uint32_t u = L.unit[c];
         int q = u_owner(u);
         if (u == 0 || q < 0) continue;
-        int r = ut_sight(u_type(u)), x = c % p.W, y = c / p.W;
-        uint32_t* vq = L.vis + q * nw;
-        for (int dy = -r; dy <= r; dy++) {
-            int yy = y + dy;
-            if (yy < 0 || yy >= p.H) continue;
-            for (int dx = -r; dx <= r; dx++) {
-                int xx = x + dx;
-                if (xx < 0 || xx >= p.W || dx * dx + dy * dy > r * r) continue;
-                int cc = yy * p.W + xx;
-                atomicOr(&vq[cc >> 5], 1u << (cc & 31));
-            }
-        }
+        or_sight_disk(L.vis + q * nw, c % p.W, c / p.W, ut_sight(u_type(u)), p.W, p.H);
     }
     __syncthreads();
 }
@@ -416,6 +406,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     // aux / vis / sc.  Phase B must read nothing but the output words `ow` / `mw`
     // (their own region at fb_outw_offset) and kernel parameters.
     if ((int)threadIdx.x < skip) return;
+    MRTS_STAMP(8, (int)threadIdx.x == skip);
     __builtin_amdgcn_s_setprio(0);
     const int t0 = (int)threadIdx.x - skip, nt = NT - skip;
     if (obs) {
@@ -474,6 +465,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             }
         }
     }
+    MRTS_STAMP_MAX(9, (threadIdx.x & 63) == 0);
 }
 
 // A parked game's envs read zero: mask / source rows (when p.mask is set), and
@@ -883,6 +875,18 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     // barriers) over other workgroups' output streams (memory-bound), which
     // drop to 0 in emit_outputs' phase B
     __builtin_amdgcn_s_setprio(2);
+#ifdef MRTS_STAMPS
+    if (threadIdx.x == 0) {
+        mrts_stamp_row = (int)atomicAdd(&g_stamp_n, 1u);
+        if (mrts_stamp_row < MRTS_STAMP_ROWS) {
+            g_stamp[mrts_stamp_row][0] = (unsigned long long)g | ((unsigned long long)HW << 32);
+            g_stamp[mrts_stamp_row][1] = (unsigned long long)(g >= p.nsp_games) | ((unsigned long long)(FB && NT > 64) << 1) |
+                                         ((unsigned long long)p.early_bot << 2);
+        }
+    }
+    __syncthreads();
+#endif
+    MRTS_STAMP(2, threadIdx.x == 0);
     const Grid gd{p.W, p.H, HW};
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
     StatePf pf;
@@ -915,6 +919,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
         for (int c = threadIdx.x; c < HW; c += NT) L.resv[c] = -1;
         load_game<NT>(p, L, g);
     }
+    MRTS_STAMP(3, threadIdx.x == 0);
     const int time = L.sc[SC_TIME];
     const int steps0 = L.sc[SC_STEPS], map_now = L.sc[SC_MAP];   // read before any lane can rewrite them (auto-reset)
     // bot-vs-bot game (MicroRTSBotVecEnv): player 0's PlayerAction comes from k_bot too
@@ -1043,6 +1048,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     }
     // (2b) the ordered path for the rest
     int nrows = compact_cells<NT>(HW, [&](int c) { return (L.aux[c] & CAND) != 0; }, L.list, L.ballot);
+    MRTS_STAMP(4, threadIdx.x == 0);
     // (2) ordered part: p0 then p1 (bot envs: the passive bot issues only NONEs)
     if (threadIdx.x == 0) {
         L.sc[SC_NPROD] = nprod;
@@ -1052,6 +1058,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
         else if (npa > 0) issue_player(p, L, gd, 1, L.blist, npa, false);
     }
     __syncthreads();
+    MRTS_STAMP(5, threadIdx.x == 0);
     // (3) fillWithNones(gs, player, 1) for every idle unit (both players); the
     //     cycle's first passes below read each cell on the lane that wrote it.
     //     claim[0, posw) (dead since the decode's claims) is cleared for the ready
@@ -1106,6 +1113,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     if (nprodr) atomicAdd(&L.sc[SC_RPROD], nprodr);   // the ids the produced units take (SC_RPROD starts at 0)
     const int uid0 = L.sc[SC_UID];   // read before lane 0 may advance it (below)
     serial = __syncthreads_or(serial);
+    MRTS_STAMP(6, threadIdx.x == 0);
     if (serial) {
         if (threadIdx.x == 0)
             for (int i = 0; i < nready; i++) execute_one(L, gd, L.snap[i]);
@@ -1171,6 +1179,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     }
     __syncthreads();
     // (7) write back + one-hot observation of every view
+    MRTS_STAMP(7, threadIdx.x == 0);
     store_game<NT>(p, L, g);
     // + getMasks of the next tick (bound mask outputs): every read of this
     //   game's source rows (phase 1) is behind the barriers above
@@ -1191,11 +1200,13 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
         __syncthreads();
         bot_setup_workgroup<NT>(p, smem, tail, L.wall, L.ballot);
         __syncthreads();
+        MRTS_STAMP(14, threadIdx.x == 0);
     }
     if (!early || threadIdx.x >= 64) emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0, early ? early_cnt : nullptr);
     if (FB && botg && threadIdx.x < 64) {
         if (early) __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
         bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, tail, early ? L.wall : nullptr, early);
+        MRTS_STAMP(13, threadIdx.x == 0);
     }
 }
 
@@ -1637,6 +1648,27 @@ static hipError_t step_group(const EngineParams* ps, int n, hipStream_t s, bool 
 }  // namespace mrts
 
 extern "C" {
+#ifdef MRTS_STAMPS
+// experiment builds: copy the stamp rows of the launches since the last reset
+// (reset != 0 zeroes the rows and the row counter first); returns the row count
+int mrts_debug_stamps(unsigned long long* out, int max_rows, int reset) {
+    unsigned int n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_stamp_n), sizeof n, 0, hipMemcpyDeviceToHost)) return -1;
+    n = n < (unsigned)MRTS_STAMP_ROWS ? n : (unsigned)MRTS_STAMP_ROWS;
+    const int rows = (int)n < max_rows ? (int)n : max_rows;
+    if (out && rows > 0 &&
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * MRTS_STAMP_COLS * rows, 0, hipMemcpyDeviceToHost))
+        return -1;
+    if (reset) {
+        static unsigned long long zero[1024][MRTS_STAMP_COLS];
+        for (int r = 0; r < MRTS_STAMP_ROWS; r += 1024)
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), zero, sizeof zero, sizeof zero * (r / 1024), hipMemcpyHostToDevice)) return -1;
+        const unsigned int z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_n), &z, sizeof z, 0, hipMemcpyHostToDevice)) return -1;
+    }
+    return rows;
+}
+#endif
 hipError_t mrts_engine_reset(const EngineParams* p, hipStream_t s, const int32_t* games, const int32_t* maps, int count) {
     return mrts::dispatch(*p, 0, s, games, maps, count);
 }

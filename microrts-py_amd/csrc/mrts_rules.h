@@ -33,6 +33,25 @@ __device__ __forceinline__ int ut_harvest_amount(int) { return 1; }
 __device__ __forceinline__ int ut_sight(int t) {
     return t == BASE ? 5 : (t == BARRACKS || t == WORKER || t == RANGED) ? 3 : (t == LIGHT || t == HEAVY) ? 2 : 0;
 }
+// PartiallyObservableGameState: OR the sight disk of a unit at (x, y) (cells with
+// dx^2 + dy^2 <= r^2 inside the map) into the bitmap vq (bit c = cell c), one
+// span per row: a row's cells are consecutive bits, so each dy costs one
+// atomicOr per 32-bit word the span touches (<= 2 for W <= 32) instead of one
+// per cell (a base's 81 -> 11).
+__device__ __forceinline__ void or_sight_disk(uint32_t* vq, int x, int y, int r, int W, int H) {
+    for (int dy = -r; dy <= r; dy++) {
+        const int yy = y + dy;
+        if (yy < 0 || yy >= H) continue;
+        int w = r;
+        while (w * w + dy * dy > r * r) w--;   // the row's half-width (r <= 5)
+        const int b0 = yy * W + max(x - w, 0), b1 = yy * W + min(x + w, W - 1);   // inclusive bit span
+        for (int wd = b0 >> 5; wd <= (b1 >> 5); wd++) {
+            const int lo = max(b0 - 32 * wd, 0), hi = min(b1 - 32 * wd, 31);
+            const uint32_t m = (hi - lo == 31 ? 0xFFFFFFFFu : ((1u << (hi - lo + 1)) - 1u)) << lo;
+            atomicOr(&vq[wd], m);
+        }
+    }
+}
 __device__ __forceinline__ bool ut_can_move(int t) { return t >= WORKER; }
 __device__ __forceinline__ bool ut_can_attack(int t) { return t >= WORKER; }
 __device__ __forceinline__ bool ut_can_harvest(int t) { return t == WORKER; }
