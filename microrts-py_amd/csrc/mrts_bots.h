@@ -74,10 +74,13 @@ __host__ __device__ inline size_t bot_tail_bytes(int HW, int W) {
     const size_t posw = (size_t)(HW + 2 * W) / 32 + 1;
     return 2 * b16(4 * posw) + b16(4 * ((size_t)HW / 32 + 1)) + b16(4 * 4) + b16(4 * bot_fw_words(HW));
 }
+// unit uid act ucell uuid pa + the abstract actions (the fused step's region)
+__host__ __device__ inline size_t bot_core_bytes(int HW) { return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW); }
 __host__ __device__ inline size_t bot_lds_bytes(int HW, int W) {
-    return b16(4 * (size_t)HW) * 6 + b16(32 * (size_t)HW) + b16((size_t)HW) + bot_tail_bytes(HW, W);
+    return bot_core_bytes(HW) + b16((size_t)HW) + bot_tail_bytes(HW, W);
 }
-__host__ __device__ inline BL bot_carve(unsigned char* base, int HW, int W, unsigned char* tail = nullptr) {
+// own_wall = false: no terrain slot (the fused bot reads the step's terrain in place)
+__host__ __device__ inline BL bot_carve(unsigned char* base, int HW, int W, unsigned char* tail = nullptr, bool own_wall = true) {
     BL L;
     size_t o = 0;
     auto take = [&](size_t n) { unsigned char* p = base + o; o += b16(n); return p; };
@@ -89,7 +92,7 @@ __host__ __device__ inline BL bot_carve(unsigned char* base, int HW, int W, unsi
     L.uuid = (int32_t*)take(4 * (size_t)HW);
     L.pa = (int32_t*)take(4 * (size_t)HW);
     L.aa = (int4*)take(32 * (size_t)HW);
-    L.wall = (uint8_t*)take((size_t)HW);   // at the step kernel's wall offset too (wall_shared)
+    L.wall = own_wall ? (uint8_t*)take((size_t)HW) : nullptr;
     if (tail) {
         base = tail;
         o = 0;
@@ -1199,12 +1202,8 @@ __device__ __forceinline__ void bot_sync() {
 // workgroup for the NEXT tick while the other waves stream the outputs (no
 // workgroup barriers here then; the game state was stored before the caller's
 // last barrier); otherwise the body of k_bot (a one-wave workgroup).
-// the bot's wall array lies where the step kernel's does (its carve: ten arrays
-// of 4*HW bytes and the 16*HW-byte snapshots; the bot's: six of 4*HW and the
-// 32*HW-byte abstract actions): the fused bot reads the step's copy
-__host__ __device__ inline bool wall_shared(int HW) {
-    return 10 * b16(4 * (size_t)HW) + b16(16 * (size_t)HW) == 6 * b16(4 * (size_t)HW) + b16(32 * (size_t)HW);
-}
+// FUSED: `tail` (the small arrays' region) and `step_wall` (the step's terrain,
+// read in place) are the fused k_step layout's (mrts_engine.hip fb_*_offset).
 
 template <bool FUSED>
 __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int player, unsigned char* smem,
@@ -1222,9 +1221,8 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
         if (lane0()) genv[w_npa] = 0;
         return;
     }
-    BL L = bot_carve(smem, HW, W, tail);
-    // the early fused bot reads the step's terrain in place: the waves beside it
-    // read it too, and its own wall slot may overlap it (mrts_engine.hip early_bot_disjoint)
+    BL L = bot_carve(smem, HW, W, tail, step_wall == nullptr);
+    // the fused bot reads the step's terrain in place (the waves beside it read it too)
     if (step_wall) L.wall = const_cast<uint8_t*>(step_wall);
     int4* const aa_g = p.aa + ((size_t)b * 2 + player) * HW * 2;
     int32_t* const pa_g = p.botpa + ((size_t)b * 2 + player) * HW;
@@ -1248,8 +1246,8 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     // Fused: the step kernel's unit / uid / act arrays sit at the bot's offsets
     // (both carves start unit, uid, act of 4*HW bytes at smem 0) and hold the
     // state it has just stored -- no reload.
-    // Fused, its wall array too (wall_shared), and the first 128 abstract-action
-    // words come prefetched in registers (pre_aa / pre_aa2: words lane, lane + 64).
+    // Fused, the first 128 abstract-action words come prefetched in registers
+    // (pre_aa / pre_aa2: words lane, lane + 64).
     // preset (the fused k_step's early bot, full observability): the workgroup has
     // already built the pending reservations, the free-cell words and the unit list
     // (mrts_engine.hip bot_setup_workgroup) and zeroed the tail arrays
@@ -1260,7 +1258,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
             L.uid[c] = v.y;
             L.act[c] = (uint32_t)v.z;
         }
-        if (!FUSED || (!step_wall && !wall_shared(HW))) L.wall[c] = p.map_wall[(size_t)map * HW + c];
+        if (!step_wall) L.wall[c] = p.map_wall[(size_t)map * HW + c];
     }
     for (int i = lane; !preset && i < posw; i += BT) L.pend[i] = L.pab[i] = 0;
     for (int i = lane; !preset && i < visw; i += BT) L.vis[i] = 0;

@@ -362,7 +362,7 @@ static bool bound(mrts_vec *h) { return h && h->ws; }
 // workgroup (the fused step workgroup has at least two waves: maps of <= 64
 // cells take 128 lanes, mrts_engine.hip step_nt).
 static bool fused(const mrts_vec *h) {
-    return h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && mrts_engine_fused_lds_bytes(h->HW, h->W) <= 163840;
+    return h->fuse && h->nbot_active > 0 && h->nbot0 == 0 && mrts_engine_fused_lds_bytes(h->HW, h->W, h->partial_obs) <= 163840;
 }
 
 // k_bot (when the tick's bot decisions are not already there) + k_step on s
@@ -472,17 +472,20 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
     return e ? hip_fail(h, e, "step launch") : MRTS_OK;
 }
 
-// A member may share a launch when its workgroup still leaves >= 4 per CU at the
-// widest workgroup size (a larger map -- 24x24 fused: 52 KB -- keeps its own
-// launch, or it would cut every member's residency to its own).
-static const size_t kGroupLdsCap = 163840 / 4;
+// A member may share a launch when its workgroup still leaves >= this many per CU
+// at the widest workgroup size (a larger map keeps its own launch, or it would cut
+// every member's residency to its own).
+#ifndef MRTS_GROUP_MIN_WG_PER_CU
+#define MRTS_GROUP_MIN_WG_PER_CU 4
+#endif
+static const size_t kGroupLdsCap = 163840 / MRTS_GROUP_MIN_WG_PER_CU;
 
 // Launch plan of a group: launch_of[i] = the launch (0, 1, ..) member i runs in.
 // Members of equal planes / obs type / fusion share a launch (merge != 0), each
 // launch in the caller's order of its first member.  Returns the launch count.
 static int group_plan(const EngineParams *ps, int n, int policy, int *launch_of) {
     const int merge = policy & 3;
-    auto lds = [&](const EngineParams &p, int NT) { return mrts_engine_group_lds_bytes(p.HW, p.W, p.fuse_bots, NT); };
+    auto lds = [&](const EngineParams &p, int NT) { return mrts_engine_group_lds_bytes(p.HW, p.W, p.fuse_bots, NT, p.partial_obs); };
     auto compatible = [&](const EngineParams &a, const EngineParams &b) {
         return a.partial_obs == b.partial_obs && a.obs_float == b.obs_float && (a.fuse_bots != 0) == (b.fuse_bots != 0);
     };
@@ -744,7 +747,7 @@ int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out) {
 int mrts_fused_layout_ok(int32_t width, int32_t height) {
     if (width <= 0 || height <= 0 || width > 32 || height > 64) return -1;
     const int HW = width * height;
-    if (mrts_engine_fused_lds_bytes(HW, width) > 163840) return -1;
+    if (mrts_engine_fused_lds_bytes(HW, width, 0) > 163840) return -1;
     if (mrts_engine_bot_lds_bytes(HW, width) > 65536) return -1;   // mrts_create refuses such bot engines
     return mrts_engine_early_bot_ok(HW, width);
 }

@@ -79,7 +79,7 @@ hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t
 hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step_group(const EngineParams *ps, int n, hipStream_t s, int bots_first);
-size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT);
+size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT, int partial);
 int mrts_engine_step_nt(int HW, int fused);
 hipError_t mrts_engine_bots(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *raw);
@@ -89,7 +89,7 @@ hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n
 hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, int map, int size, uint8_t *rgb);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);
-size_t mrts_engine_fused_lds_bytes(int HW, int W);
+size_t mrts_engine_fused_lds_bytes(int HW, int W, int partial);
 int mrts_engine_early_bot_ok(int HW, int W);
 }
 #endif

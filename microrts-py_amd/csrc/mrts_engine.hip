@@ -48,7 +48,8 @@ struct Lds {
     int32_t* blist;  // the bot's PlayerAction order (bot games)
     int32_t* blist0; // player 0's bot PlayerAction (bot-vs-bot games)
     int4* snap;      // ready-action snapshots
-    uint32_t* outw;  // emit_outputs words: aliases resv .. snap (32 B per cell)
+    uint32_t* outw;  // emit_outputs one-hot words [NV][HW]: aliases resv .. snap (32 B per cell with outm)
+    uint32_t* outm;  // emit_outputs mask words [NV][HW][3] (outw + 2 HW, unless the fused step places them)
     uint8_t* wall;
     unsigned long long* ballot;
     uint32_t* posbits;
@@ -61,7 +62,9 @@ enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_U
        SC_STEPS = MRTS_G_STEPS, SC_MAP = MRTS_G_MAP, SC_ERR = MRTS_G_ERR, SC_AA_N = MRTS_G_AA_N, SC_TICKS = MRTS_G_TICKS,
        SC_NPA = MRTS_G_NPA, SC_R0 = 16, /* rewards: [player][6] as ints */ SC_NPROD = 28, SC_RPROD = 29 /* ready produces */,
        SC_OVER = 30 /* a pending produce is over its owner's budget */,
-       SC_HAS = 31 /* units of player 0 (bits 0..15) and player 1 (16..31) */, SC_WORDS = 32 };
+       SC_HAS = 31 /* units of player 0 (bits 0..15) and player 1 (16..31) */,
+       SC_PSUM = 32 /* [2] cost of the player's produce rows this tick */,
+       SC_PMAX = 34 /* [2] largest cost among the player's pending produces */, SC_WORDS = 36 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -83,11 +86,14 @@ __host__ __device__ inline size_t vis_bytes(int HW, int NT) {
     return v > b ? v : b;
 }
 
-__host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
+// b0: the blist0 array (player 0's bot PlayerAction: bot-vs-bot games, which are
+// never bot-fused); wall: the terrain array (the fused step keeps it apart, at
+// fb_wall_offset)
+__host__ __device__ inline size_t lds_bytes(int HW, int W, int NT, bool b0 = true, bool wall = true) {
     size_t b = 0;
-    b += a16(4 * (size_t)HW) * 10; // unit uid act seq aux resv list prod blist blist0
+    b += a16(4 * (size_t)HW) * (b0 ? 10 : 9); // unit uid act seq aux resv list prod blist [blist0]
     b += a16(16 * (size_t)HW);     // snap
-    b += a16((size_t)HW);          // wall
+    b += wall ? a16((size_t)HW) : 0;
     b += a16(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     b += a16(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     b += a16(4 * SC_WORDS);
@@ -96,21 +102,38 @@ __host__ __device__ inline size_t lds_bytes(int HW, int W, int NT) {
     return b;
 }
 
-// Bot-fused k_step layout: [0, max(step, bot)) holds the step's arrays until
-// phase A's barrier and the bot's afterwards; the output words (one-hot + mask
-// bits, 32 B per cell for two views) get their own region behind it, so waves
-// 1.. can stream them while wave 0 reuses the rest.
+// Bot-fused k_step layout (24x24 52.3 KB -> 40.1 KB, 3 -> 4
+// workgroups per CU):
+//   [0, core)   the step's arrays (no blist0, no terrain) until phase A, the
+//               bot's (unit uid act ucell uuid pa, abstract actions) afterwards
+//   outw        a bot game's output words: it streams them while wave 0 runs the
+//               bot, so they lie outside the bot's region -- its mask words (one
+//               view, 12 B per cell) here, its one-hot words (4 B per cell) in the
+//               step's uid array on the early path (the bot reads uids only in its
+//               setup, which the workgroup builds before the waves split), else
+//               here behind the mask words
+//   tail        the bot's small arrays (pend pab vis sc fw)
+//   counter     the streaming waves' phase-A meeting point (early path)
+//   wall        the terrain, read in place by the step, phase A and the bot
+// Selfplay games of a fused launch run no bot and alias their output words onto
+// the step's dead arrays, as the unfused kernel does.  `early`: the engine takes
+// the early path (full observability and early_bot_disjoint).
 __host__ __device__ inline size_t fb_outw_offset(int HW, int W, int NT) {
-    const size_t a = lds_bytes(HW, W, NT), b = bots::bot_lds_bytes(HW, W);
+    const size_t a = lds_bytes(HW, W, NT, false, false), b = bots::bot_core_bytes(HW);
     return a16(a > b ? a : b);
 }
-// + the early bot's (P == 29) tail arrays and the streaming waves' phase-A counter
-__host__ __device__ inline size_t fb_tail_offset(int HW, int W, int NT) { return fb_outw_offset(HW, W, NT) + a16(32 * (size_t)HW); }
-__host__ __device__ inline size_t fb_lds_bytes(int HW, int W, int NT) {
-    return fb_tail_offset(HW, W, NT) + a16(bots::bot_tail_bytes(HW, W)) + 16;
+__host__ __device__ inline size_t fb_tail_offset(int HW, int W, int NT, bool early) {
+    return fb_outw_offset(HW, W, NT) + a16((early ? 12 : 16) * (size_t)HW);
+}
+__host__ __device__ inline size_t fb_early_cnt_offset(int HW, int W, int NT, bool early) {
+    return fb_tail_offset(HW, W, NT, early) + a16(bots::bot_tail_bytes(HW, W));
+}
+__host__ __device__ inline size_t fb_wall_offset(int HW, int W, int NT, bool early) { return fb_early_cnt_offset(HW, W, NT, early) + 16; }
+__host__ __device__ inline size_t fb_lds_bytes(int HW, int W, int NT, bool early) {
+    return fb_wall_offset(HW, W, NT, early) + a16((size_t)HW);
 }
 
-__host__ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT) {
+__host__ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT, bool b0 = true, uint8_t* wall = nullptr) {
     Lds L;
     size_t o = 0;
     auto take = [&](size_t n) { unsigned char* p = base + o; o += a16(n); return p; };
@@ -123,10 +146,12 @@ __host__ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT)
     L.list = (int32_t*)take(4 * (size_t)HW);
     L.prod = (int32_t*)take(4 * (size_t)HW);
     L.blist = (int32_t*)take(4 * (size_t)HW);
-    L.blist0 = (int32_t*)take(4 * (size_t)HW);
+    // (!b0: unreachable by construction -- fused engines have no player-0 bots, mrts_capi fused())
+    L.blist0 = b0 ? (int32_t*)take(4 * (size_t)HW) : L.blist;
     L.snap = (int4*)take(16 * (size_t)HW);
-    L.outw = (uint32_t*)L.resv;   // resv, list, prod, blist, blist0, snap: >= 36 B per cell, contiguous
-    L.wall = (uint8_t*)take((size_t)HW);
+    L.outw = (uint32_t*)L.resv;   // resv, list, prod, blist, [blist0,] snap: >= 32 B per cell, contiguous
+    L.outm = L.outw + 2 * HW;
+    L.wall = wall ? wall : (uint8_t*)take((size_t)HW);
     L.ballot = (unsigned long long*)take(8 * (size_t)((HW + NT - 1) / NT) * (NT / 64) + 8);
     L.posbits = (uint32_t*)take(4 * (size_t)((HW + 2 * W + 31) / 32 + 1));
     L.sc = (int*)take(4 * SC_WORDS);
@@ -136,20 +161,18 @@ __host__ __device__ inline Lds carve(unsigned char* base, int HW, int W, int NT)
 }
 
 // The early-bot k_step (FB, P == 29): while wave 0 runs bots::bot_game (its
-// small arrays in the tail region, the step's terrain read in place), waves 1..
-// run emit_outputs' phase A, which reads the step's unit / act / wall / scalars
-// and writes the output words and the meeting counter.  True when, for this map
-// size, the bot writes none of those bytes and phase A writes none the bot reads
-// -- computed from the two carves themselves -- and the bot's unit / uid / act
-// arrays are the step's (it reads the state just stored in place).  The host
+// small arrays in the tail region, the step's terrain read in place, setup
+// preset), waves 1.. run emit_outputs' phase A, which reads the step's unit / act
+// / wall / scalars and writes the output words (one-hot into the uid array, mask
+// words behind the bot's region) and the meeting counter.  True when, for this
+// map size, the bot writes none of those bytes and phase A writes none the bot
+// reads -- computed from the two carves themselves -- and the bot's unit / uid /
+// act arrays are the step's (it reads the state just stored in place).  The host
 // takes the early path only then (EngineParams::early_bot; mrts_fused_layout_ok).
-__host__ __device__ inline size_t fb_early_cnt_offset(int HW, int W, int NT) {
-    return fb_tail_offset(HW, W, NT) + a16(bots::bot_tail_bytes(HW, W));
-}
 __host__ __device__ inline bool early_bot_disjoint(int HW, int W, int NT) {
     unsigned char* const z = reinterpret_cast<unsigned char*>((size_t)1 << 20);   // any base: only offsets matter
-    const Lds S = carve(z, HW, W, NT);
-    const bots::BL B = bots::bot_carve(z, HW, W, z + fb_tail_offset(HW, W, NT));
+    const Lds S = carve(z, HW, W, NT, false, z + fb_wall_offset(HW, W, NT, true));
+    const bots::BL B = bots::bot_carve(z, HW, W, z + fb_tail_offset(HW, W, NT, true), false);
     struct R {
         const void* p;
         size_t n;
@@ -161,11 +184,11 @@ __host__ __device__ inline bool early_bot_disjoint(int HW, int W, int NT) {
     const R bot_w[9] = {{B.ucell, 4 * hw}, {B.uuid, 4 * hw}, {B.pa, 4 * hw}, {B.aa, 32 * hw},
                         {B.pend, 4 * posw}, {B.pab, 4 * posw}, {B.vis, 4 * visw}, {B.sc, 16},
                         {B.fw, 4 * bots::bot_fw_words(HW)}};
-    const R bot_r[4] = {{B.unit, 4 * hw}, {B.uid, 4 * hw}, {B.act, 4 * hw}, {S.wall, hw}};
-    const R a_r[4] = {{S.unit, 4 * hw}, {S.act, 4 * hw}, {S.wall, hw}, {S.sc, 4 * (size_t)SC_WORDS}};
-    const R a_w[2] = {{z + fb_outw_offset(HW, W, NT), 32 * hw}, {z + fb_early_cnt_offset(HW, W, NT), 4}};
+    const R bot_r[3] = {{B.unit, 4 * hw}, {B.act, 4 * hw}, {S.wall, hw}};   // (uids: read by the setup only)
+    const R a_r[3] = {{S.unit, 4 * hw}, {S.act, 4 * hw}, {S.wall, hw}};      // (resources: in registers)
+    const R a_w[3] = {{S.uid, 4 * hw}, {z + fb_outw_offset(HW, W, NT), 12 * hw}, {z + fb_early_cnt_offset(HW, W, NT, true), 4}};
     for (const R& b : bot_w) {
-        if (lo(b) + b.n > fb_lds_bytes(HW, W, NT)) return false;
+        if (lo(b) + b.n > fb_lds_bytes(HW, W, NT, true)) return false;
         for (const R& a : a_r) if (overlap(a, b)) return false;
         for (const R& a : a_w) if (overlap(a, b)) return false;
     }
@@ -226,7 +249,7 @@ template <int NT>
 __device__ __forceinline__ void bot_setup_workgroup(const EngineParams& p, unsigned char* smem, unsigned char* tail,
                                                     const uint8_t* wall, unsigned long long* scratch) {
     const int HW = p.HW, W = p.W, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const bots::BL B = bots::bot_carve(smem, HW, W, tail);
+    const bots::BL B = bots::bot_carve(smem, HW, W, tail, false);
     for (int base = 0; base < HW; base += NT) {
         const int c = base + (int)threadIdx.x;
         bool fr = false;
@@ -358,12 +381,14 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
 // `early_cnt` (the early-bot k_step): wave 0 is running the bot already, so
 // phase A too runs on lanes [skip, NT) only and its end is a counter the
 // streaming waves meet at in LDS instead of a workgroup barrier.
+// res0 / res1: the players' resources (the masks' produce checks), read by the
+// caller from L.sc before the early bot may overwrite the step's scalars.
 template <int NT, int P, typename OT>
-__device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks,
-                                             int skip = 0, int* early_cnt = nullptr) {
+__device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks, int res0,
+                                             int res1, int skip = 0, int* early_cnt = nullptr) {
     const int HW = p.HW, NV = G.nviews;
-    uint32_t* ow = L.outw;            // [NV][HW]    one-hot bits
-    uint32_t* mw = L.outw + 2 * HW;   // [NV][HW][3] mask bits (bit 0 = source)
+    uint32_t* ow = L.outw;   // [NV][HW]    one-hot bits
+    uint32_t* mw = L.outm;   // [NV][HW][3] mask bits (bit 0 = source)
     const Grid gd{p.W, p.H, HW};
     if (obs && P == 31) compute_vis<NT>(p, L);
     const int nw = HW / 32 + 1;
@@ -383,7 +408,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             }
             if (masks) {
                 uint32_t m[3];
-                cell_mask(gd, c, v, L.unit, L.act, L.wall, v == 0 ? L.sc[SC_RES0] : L.sc[SC_RES1], m);
+                cell_mask(gd, c, v, L.unit, L.act, L.wall, v == 0 ? res0 : res1, m);
                 mw[3 * (v * HW + c)] = m[0];
                 mw[3 * (v * HW + c) + 1] = m[1];
                 mw[3 * (v * HW + c) + 2] = m[2];
@@ -402,9 +427,10 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     }
     // ---- phase B -----------------------------------------------------------
     // Bot-fused k_step (skip = 64): from here on wave 0 runs bots::bot_game, whose
-    // LDS region starts at smem offset 0 and overwrites L.unit / uid / act / seq /
-    // aux / vis / sc.  Phase B must read nothing but the output words `ow` / `mw`
-    // (their own region at fb_outw_offset) and kernel parameters.
+    // LDS region starts at smem offset 0 and overwrites the step's arrays but the
+    // unit / act / wall it reads and, on the early path, the uid array.  Phase B
+    // must read nothing but the output words `ow` / `mw` (fb_outw_offset) and
+    // kernel parameters.
     if ((int)threadIdx.x < skip) return;
     MRTS_STAMP(8, (int)threadIdx.x == skip);
     __builtin_amdgcn_s_setprio(0);
@@ -510,7 +536,7 @@ __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* gam
     __syncthreads();
     store_game<NT>(p, L, g);
     Game G = game_of(p, g);
-    emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr);
+    emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, L.sc[SC_RES0], L.sc[SC_RES1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -561,7 +587,7 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
         return;
     }
     load_game<NT>(p, L, g);
-    emit_outputs<NT, 29, int32_t>(p, L, game_of(p, g), false, true);
+    emit_outputs<NT, 29, int32_t>(p, L, game_of(p, g), false, true, L.sc[SC_RES0], L.sc[SC_RES1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -867,9 +893,15 @@ template <int NT, int P, typename OT, bool FB>
 __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int HW = p.HW;
-    Lds L = carve(smem, HW, p.W, NT);
-    if (FB) L.outw = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
-    int* const early_cnt = reinterpret_cast<int*>(smem + fb_early_cnt_offset(HW, p.W, NT));
+    const bool early_layout = FB && P == 29 && p.early_bot;
+    Lds L = carve(smem, HW, p.W, NT, !FB, FB ? smem + fb_wall_offset(HW, p.W, NT, early_layout) : nullptr);
+    const bool botg = FB && g >= p.nsp_games && NT > 64;   // the workgroup runs the next tick's bot
+    if (botg) {   // the output words outside the bot's region (fb_outw_offset)
+        uint32_t* const region = reinterpret_cast<uint32_t*>(smem + fb_outw_offset(HW, p.W, NT));
+        L.outw = early_layout ? reinterpret_cast<uint32_t*>(L.uid) : region;
+        L.outm = early_layout ? region : region + HW;
+    }
+    int* const early_cnt = reinterpret_cast<int*>(smem + fb_early_cnt_offset(HW, p.W, NT, early_layout));
     if (FB && threadIdx.x == 0) *early_cnt = 0;   // read after several barriers below
     // issue priority: the game logic (latency-bound chains of LDS steps and
     // barriers) over other workgroups' output streams (memory-bound), which
@@ -893,7 +925,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     if (game_parked(p, g)) return;   // no tick: its outputs stay zero (mrts_park_games)
     if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
     if (FB && P == 29 && p.early_bot && g >= p.nsp_games && NT > 64) {   // the early bot's tail arrays start zeroed
-        uint32_t* t = reinterpret_cast<uint32_t*>(smem + fb_tail_offset(HW, p.W, NT));
+        uint32_t* t = reinterpret_cast<uint32_t*>(smem + fb_tail_offset(HW, p.W, NT, true));
         for (int i = threadIdx.x; i < (int)(bots::bot_tail_bytes(HW, p.W) / 4); i += NT) t[i] = 0;
     }
     const Game G = game_of(p, g);
@@ -941,7 +973,11 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
             if (ty == A_MOVE || ty == A_PRODUCE) {
                 const int n = nb_cell(gd, c, code_param(code));
                 if (n >= 0) L.resv[n] = c;
-                if (ty == A_PRODUCE && ut_cost(code_utype(code)) > res_of(L, u_owner(u))) L.sc[SC_OVER] = 1;
+                if (ty == A_PRODUCE) {
+                    const int cost = ut_cost(code_utype(code));
+                    if (cost > res_of(L, u_owner(u))) L.sc[SC_OVER] = 1;
+                    if (ow == 0 || ow == 1) atomicMax(&L.sc[SC_PMAX + ow], cost);
+                }
             }
         }
         if (u != 0 && ow >= 0 && pa == 0) {
@@ -970,6 +1006,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                         bool lg = legal_code(gd, c, code, L.unit, L.wall, res_of(L, ow));
                         nw = CAND | (lg ? LEGAL : 0u) | (uint32_t)code;
                         claim_target(L, gd, c, code, posw);
+                        if (code_type(code) == A_PRODUCE) atomicAdd(&L.sc[SC_PSUM + ow], ut_cost(code_utype(code)));
                     }
                 }
             }
@@ -994,6 +1031,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
             L.aux[c] = CAND | (legal_code(gd, c, code, L.unit, L.wall, res_of(L, q)) ? LEGAL : 0u) | ((uint32_t)k << 12) |
                        (uint32_t)code;
             claim_target(L, gd, c, code, posw);
+            if (code_type(code) == A_PRODUCE) atomicAdd(&L.sc[SC_PSUM + q], ut_cost(code_utype(code)));
         }
     }
     // (the compaction's barrier orders the reservations, claims, SC_OVER and the
@@ -1005,14 +1043,21 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
         return a != 0 && code_type(act_code(a)) == A_PRODUCE;
     }, L.prod, reinterpret_cast<unsigned long long*>(L.vis));
     // (2a) rows that interact with nothing else this tick issue lane-parallel: a
-    //      row (agent or device bot) that is not a produce and, if a move, whose
-    //      target position no other row (either player) and no pending assignment
-    //      claims, while no pending produce is over its owner's budget (which would
-    //      make every new action inconsistent).  Such a row meets no candidate in
-    //      issue() and no other row in fromVectorAction's filter, and no ordered
-    //      row of the other player meets it, so issuing it out of order is exact:
-    //      its LinkedHashMap rank is still its cell (agent rows) or its position in
-    //      the bot's PlayerAction.  Everything else takes the ordered path (2b).
+    //      row (agent or device bot) whose target position, if a move or produce,
+    //      no other row (either player) and no pending assignment claims, while no
+    //      pending produce is over its owner's budget (which would make every new
+    //      action inconsistent); a produce besides only while all of its player's
+    //      produce rows this tick together with the player's dearest pending
+    //      produce fit the player's resources (SC_PSUM + SC_PMAX): then no prefix of
+    //      the PlayerAction's ResourceUsage exceeds them (fromVectorAction keeps it
+    //      and every later row) and no pair of produces is over budget (issue()
+    //      finds no candidate for it, nor does any later row find it).  Such a row
+    //      meets no candidate in issue() and no other row in fromVectorAction's
+    //      filter, and no ordered row of either player meets it, so issuing it out
+    //      of order is exact: its LinkedHashMap rank is still its cell (agent rows)
+    //      or its position in the bot's PlayerAction.  (A parallel produce is never
+    //      a candidate of an ordered row, so it stays out of L.prod.)  Everything
+    //      else takes the ordered path (2b).
     {
         if (!L.sc[SC_OVER]) {
             for (int c = threadIdx.x; c < HW; c += NT) {
@@ -1023,9 +1068,9 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                 const bool botrow = !G.selfplay && (q != 0 || bot0);
                 const int rank = botrow ? (int)((nw >> 12) & 0xFFFu) : c;
                 const int code = (int)(nw & 0xFFFu), ty = code_type(code);
-                if (ty == A_PRODUCE) continue;
+                if (ty == A_PRODUCE && L.sc[SC_PSUM + q] + L.sc[SC_PMAX + q] > res_of(L, q)) continue;
                 int n = -1;
-                if (ty == A_MOVE) {
+                if (ty == A_MOVE || ty == A_PRODUCE) {
                     const int b = unchecked_pos(gd, c, code_param(code)) + p.W;
                     if ((L.claim[posw + (b >> 5)] >> (b & 31)) & 1u) continue;
                     n = nb_cell(gd, c, code_param(code));
@@ -1037,9 +1082,13 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                 const int ct = code_type(cur);
                 L.act[c] = act_make(cur, ct == A_NONE ? time + dur : time + eta_code(cur, u_type(u)));
                 L.seq[c] = seq_make(time, q, rank);
-                if (ct == A_MOVE) L.resv[n] = c;
+                if (ct == A_MOVE || ct == A_PRODUCE) L.resv[n] = c;
                 if (ct == A_HARVEST || ct == A_RETURN) atomicAdd(&L.sc[SC_R0 + 6 * q + 1], 1);
                 if (ct == A_ATTACK) atomicAdd(&L.sc[SC_R0 + 6 * q + 4], 1);
+                if (ct == A_PRODUCE) {   // ai.reward.ProduceWorker / ProduceBuilding / ProduceCombatUnit
+                    const int pu = code_utype(cur);
+                    atomicAdd(&L.sc[SC_R0 + 6 * q + (pu == WORKER ? 2 : (pu == BASE || pu == BARRACKS) ? 3 : 5)], 1);
+                }
                 L.aux[c] = nw & ~CAND;   // issued
             }
             // no barrier: the compaction below reads each cell's aux word on the
@@ -1181,9 +1230,9 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     // (7) write back + one-hot observation of every view
     MRTS_STAMP(7, threadIdx.x == 0);
     store_game<NT>(p, L, g);
+    const int res0 = L.sc[SC_RES0], res1 = L.sc[SC_RES1];   // before the early bot may reuse the scalars' bytes
     // + getMasks of the next tick (bound mask outputs): every read of this
     //   game's source rows (phase 1) is behind the barriers above
-    const bool botg = FB && g >= p.nsp_games && NT > 64;
     // Early bot (P == 29, p.early_bot: full observability, and for this size the bot
     // writes none of the arrays phase A reads -- unit / act / wall stay as stored, the
     // step's scalars and visibility words are left alone, its small arrays go to the
@@ -1194,18 +1243,19 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     // the bot behind its barrier (the step's arrays are dead by then: only L.outw is
     // read on).  One bot_game call site for both: the inlined bot is most of this
     // kernel's code.
-    const bool early = FB && P == 29 && botg && p.early_bot;
-    unsigned char* const tail = early ? smem + fb_tail_offset(HW, p.W, NT) : nullptr;
+    const bool early = early_layout && botg;
+    unsigned char* const tail = smem + fb_tail_offset(HW, p.W, NT, early_layout);
     if (early) {
         __syncthreads();
         bot_setup_workgroup<NT>(p, smem, tail, L.wall, L.ballot);
         __syncthreads();
         MRTS_STAMP(14, threadIdx.x == 0);
     }
-    if (!early || threadIdx.x >= 64) emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, botg ? 64 : 0, early ? early_cnt : nullptr);
+    if (!early || threadIdx.x >= 64)
+        emit_outputs<NT, P, OT>(p, L, G, true, p.mask != nullptr, res0, res1, botg ? 64 : 0, early ? early_cnt : nullptr);
     if (FB && botg && threadIdx.x < 64) {
         if (early) __builtin_amdgcn_s_setprio(3);   // the latency-bound bot wave first; the streaming waves are memory-bound
-        bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, tail, early ? L.wall : nullptr, early);
+        bots::bot_game<true>(p, g - p.nsp_games, 1, smem, L.sc, pf_ok, pf.aa, pf.aa2, tail, L.wall, early);
         MRTS_STAMP(13, threadIdx.x == 0);
     }
 }
@@ -1578,7 +1628,7 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
     } else {
         const bool fb = p.fuse_bots && NT > 64;
-        if (fb) sh = fb_lds_bytes(p.HW, p.W, NT);
+        if (fb) sh = fb_lds_bytes(p.HW, p.W, NT, !p.partial_obs && p.early_bot);
         launch_step<NT>(one_engine(p), grid, sh, s, p.partial_obs, p.obs_float, fb);
     }
     return hipGetLastError();
@@ -1618,7 +1668,7 @@ static hipError_t step_group(const EngineParams* ps, int n, hipStream_t s, bool 
         EngineParams& e = sg.e[i];
         e = ps[i];
         if (fused) e.early_bot = early_bot_disjoint(e.HW, e.W, NT) ? 1 : 0;   // the layout at this launch's NT
-        sh = std::max(sh, fused ? fb_lds_bytes(e.HW, e.W, NT) : lds_bytes(e.HW, e.W, NT));
+        sh = std::max(sh, fused ? fb_lds_bytes(e.HW, e.W, NT, !e.partial_obs && e.early_bot) : lds_bytes(e.HW, e.W, NT));
     }
     if (sh > 163840) return hipErrorInvalidValue;   // one workgroup's LDS on a CU
     int grid = 0;
@@ -1685,8 +1735,8 @@ hipError_t mrts_engine_step(const EngineParams* p, hipStream_t s) { return mrts:
 hipError_t mrts_engine_step_group(const EngineParams* ps, int n, hipStream_t s, int bots_first) {
     return mrts::step_group(ps, n, s, bots_first != 0);
 }
-size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT) {
-    return fused ? mrts::fb_lds_bytes(HW, W, NT) : mrts::lds_bytes(HW, W, NT);
+size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT, int partial) {
+    return fused ? mrts::fb_lds_bytes(HW, W, NT, !partial && mrts::early_bot_disjoint(HW, W, NT)) : mrts::lds_bytes(HW, W, NT);
 }
 int mrts_engine_step_nt(int HW, int fused) { return mrts::step_nt(HW, fused != 0); }
 hipError_t mrts_engine_sample(const int32_t* mask, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t* act, hipStream_t s) {
@@ -1713,7 +1763,10 @@ hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, in
     return hipGetLastError();
 }
 int mrts_engine_early_bot_ok(int HW, int W) { return mrts::early_bot_disjoint(HW, W, mrts::step_nt(HW, true)) ? 1 : 0; }
-size_t mrts_engine_fused_lds_bytes(int HW, int W) { return mrts::fb_lds_bytes(HW, W, mrts::step_nt(HW, true)); }
+size_t mrts_engine_fused_lds_bytes(int HW, int W, int partial) {
+    const int NT = mrts::step_nt(HW, true);
+    return mrts::fb_lds_bytes(HW, W, NT, !partial && mrts::early_bot_disjoint(HW, W, NT));
+}
 size_t mrts_engine_lds_bytes(int HW, int W) {
     int NT = HW <= 64 ? 64 : HW <= 128 ? 128 : 256;
     return mrts::lds_bytes(HW, W, NT);
