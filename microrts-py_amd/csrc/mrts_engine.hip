@@ -64,7 +64,8 @@ enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_U
        SC_OVER = 30 /* a pending produce is over its owner's budget */,
        SC_HAS = 31 /* units of player 0 (bits 0..15) and player 1 (16..31) */,
        SC_PSUM = 32 /* [2] cost of the player's produce rows this tick */,
-       SC_PMAX = 34 /* [2] largest cost among the player's pending produces */, SC_WORDS = 36 };
+       SC_PMAX = 34 /* [2] largest cost among the player's pending produces */,
+       SC_SERIAL = 36 /* the ready set executes in order */, SC_WORDS = 40 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -1161,7 +1162,11 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     }
     if (nprodr) atomicAdd(&L.sc[SC_RPROD], nprodr);   // the ids the produced units take (SC_RPROD starts at 0)
     const int uid0 = L.sc[SC_UID];   // read before lane 0 may advance it (below)
-    serial = __syncthreads_or(serial);
+    // (the OR over lanes through an LDS word: __syncthreads_or's static LDS would cost
+    // every workgroup 256 B)
+    if (serial) L.sc[SC_SERIAL] = 1;
+    __syncthreads();
+    serial = L.sc[SC_SERIAL];
     MRTS_STAMP(6, threadIdx.x == 0);
     if (serial) {
         if (threadIdx.x == 0)
