@@ -473,10 +473,12 @@ int mrts_step_weighted(mrts_vec *h, void *stream, const int64_t *actions, const 
 }
 
 // A member may share a launch when its workgroup still leaves >= this many per CU
-// at the widest workgroup size (a larger map keeps its own launch, or it would cut
-// every member's residency to its own).
+// at the widest workgroup size: the step kernels' own occupancy (6-7 workgroups
+// per CU, register-limited), so that merging costs no member residency; a larger
+// map keeps its own launch.  (configs[4], round 4: 24x24 apart at 40 KB 261 us per
+// step vs 264 us all in one launch, profiles/r04_ab/.)
 #ifndef MRTS_GROUP_MIN_WG_PER_CU
-#define MRTS_GROUP_MIN_WG_PER_CU 4
+#define MRTS_GROUP_MIN_WG_PER_CU 6
 #endif
 static const size_t kGroupLdsCap = 163840 / MRTS_GROUP_MIN_WG_PER_CU;
 

@@ -837,6 +837,56 @@ __device__ __forceinline__ void execute_one(const Lds& L, const Grid& gd, int4 s
     }
 }
 
+// Wider maps (NT < HW <= 4 NT, e.g. 24x24 and 32x32 on 256 lanes): the lane's
+// cells, their source-unit words and the terrain in registers, all issued in one
+// round trip with genv (the unprefetched path takes four: genv, cells, then the
+// sources and the actions inside the decode); the source words reach the decode
+// through L.aux.
+struct WidePf {
+    int4 cell[4];
+    int src[4];   // bit v: the source-unit word of view v
+    int wall[4];
+    int genv, map;
+    int bpa0, bpa1;   // bot games: entry `lane` of the bot PlayerActions (player 0 / 1)
+};
+template <int NT>
+__device__ __forceinline__ void prefetch_wide(const EngineParams& p, const Game& G, int g, WidePf& pf) {
+    const int HW = p.HW;
+    pf.genv = p.genv[(size_t)g * MRTS_GENV_WORDS + min((int)threadIdx.x, MRTS_GENV_WORDS - 1)];
+    pf.map = p.nmaps == 1 ? 0 : p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = min((int)threadIdx.x + k * NT, HW - 1);   // unconditional: counted waits
+        pf.cell[k] = p.cells[(size_t)g * HW + c];
+        const int s0 = p.src[(size_t)G.env0 * HW + c], s1 = p.src[(size_t)(G.env0 + G.nviews - 1) * HW + c];
+        pf.src[k] = (s0 ? 1 : 0) | (s1 ? 2 : 0);
+        if (p.nmaps == 1) pf.wall[k] = p.map_wall[c];
+    }
+    if (!G.selfplay && p.botpa) {   // speculative: the counts arrive with genv
+        const int32_t* bp = p.botpa + (size_t)(g - p.nsp_games) * 2 * HW;
+        pf.bpa0 = p.bot_ai0 ? bp[threadIdx.x] : 0;
+        pf.bpa1 = bp[HW + threadIdx.x];
+    }
+}
+template <int NT>
+__device__ __forceinline__ void commit_wide(const EngineParams& p, const Lds& L, const WidePf& pf) {
+    if (threadIdx.x < MRTS_GENV_WORDS) L.sc[threadIdx.x] = pf.genv;
+    const int HW = p.HW;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = (int)threadIdx.x + k * NT;
+        if (c >= HW) break;
+        L.unit[c] = (uint32_t)pf.cell[k].x;
+        L.uid[c] = pf.cell[k].y;
+        L.act[c] = (uint32_t)pf.cell[k].z;
+        L.seq[c] = (uint32_t)pf.cell[k].w;
+        L.wall[c] = p.nmaps == 1 ? (uint8_t)pf.wall[k] : p.map_wall[(size_t)pf.map * HW + c];
+        L.resv[c] = -1;
+        L.aux[c] = (uint32_t)pf.src[k];   // read back by the decode on this lane
+    }
+    __syncthreads();
+}
+
 // Register prefetch of a game's state (maps with HW <= NT: one cell per lane):
 // issued before the current game's output stream, so the next game's state
 // round trip overlaps those stores instead of stalling the block.
@@ -909,8 +959,10 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     // drop to 0 in emit_outputs' phase B
     __builtin_amdgcn_s_setprio(2);
 #ifdef MRTS_STAMPS
-    if (threadIdx.x == 0) {
-        mrts_stamp_row = (int)atomicAdd(&g_stamp_n, 1u);
+    if (threadIdx.x == 0) {   // rows by workgroup (no atomics: they would skew the start stamps);
+        // maps of more than 256 cells launch apart from the others (mrts_step_group plans)
+        mrts_stamp_row = (int)blockIdx.x + (HW > 256 ? MRTS_STAMP_ROWS / 2 : 0);
+        atomicMax(&g_stamp_n, (unsigned)mrts_stamp_row + 1u);
         if (mrts_stamp_row < MRTS_STAMP_ROWS) {
             g_stamp[mrts_stamp_row][0] = (unsigned long long)g | ((unsigned long long)HW << 32);
             g_stamp[mrts_stamp_row][1] = (unsigned long long)(g >= p.nsp_games) | ((unsigned long long)(FB && NT > 64) << 1) |
@@ -922,9 +974,12 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     MRTS_STAMP(2, threadIdx.x == 0);
     const Grid gd{p.W, p.H, HW};
     const bool pf_ok = HW <= NT;   // state, genv and source rows in one round trip
+    const bool pf_wide = !pf_ok && HW <= 4 * NT;   // the same for up to four cells per lane
     StatePf pf;
+    WidePf wpf;
     if (game_parked(p, g)) return;   // no tick: its outputs stay zero (mrts_park_games)
     if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
+    else if (pf_wide) prefetch_wide<NT>(p, game_of(p, g), g, wpf);
     if (FB && P == 29 && p.early_bot && g >= p.nsp_games && NT > 64) {   // the early bot's tail arrays start zeroed
         uint32_t* t = reinterpret_cast<uint32_t*>(smem + fb_tail_offset(HW, p.W, NT, true));
         for (int i = threadIdx.x; i < (int)(bots::bot_tail_bytes(HW, p.W) / 4); i += NT) t[i] = 0;
@@ -943,11 +998,13 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     if (pf_ok) {
         src_pre[0] = pf.src0;
         src_pre[1] = pf.src1;
-    } else if ((int)threadIdx.x < HW) {
+    } else if (!pf_wide && (int)threadIdx.x < HW) {
         for (int v = 0; v < G.nviews; v++) src_pre[v] = p.src[(size_t)(G.env0 + v) * HW + threadIdx.x];
     }
     if (pf_ok) {
         commit_game<NT>(p, L, pf);
+    } else if (pf_wide) {
+        commit_wide<NT>(p, L, wpf);
     } else {
         for (int c = threadIdx.x; c < HW; c += NT) L.resv[c] = -1;
         load_game<NT>(p, L, g);
@@ -985,7 +1042,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
             int view = G.selfplay ? ow : (ow == 0 && !bot0 ? 0 : -1);
             if (view >= 0) {
                 const size_t row = (size_t)(G.env0 + view) * HW + c;
-                if (c == (int)threadIdx.x ? src_pre[view] : p.src[row]) {
+                if (pf_wide ? (L.aux[c] >> view) & 1u : c == (int)threadIdx.x ? src_pre[view] : p.src[row]) {
                     const int64_t* ra = p.actions + row * 7;
                     int64_t r[7];   // all 7 components in one round trip
 #pragma unroll
@@ -1025,7 +1082,8 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     for (int q = 0; q < 2; q++) {
         const int nq = q ? npa : npa0;
         for (int k = threadIdx.x; k < nq; k += NT) {
-            const int e = (pf_ok && k == (int)threadIdx.x) ? (q ? pf.bpa1 : pf.bpa0)
+            const int e = (pf_ok && k == (int)threadIdx.x)     ? (q ? pf.bpa1 : pf.bpa0)
+                          : (pf_wide && k == (int)threadIdx.x) ? (q ? wpf.bpa1 : wpf.bpa0)
                                                            : p.botpa[((size_t)(g - p.nsp_games) * 2 + q) * HW + k];
             const int c = e & 0xFFFF, code = e >> 16;
             (q ? L.blist : L.blist0)[k] = c;

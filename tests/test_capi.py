@@ -136,11 +136,11 @@ def test_fused_early_bot_layout_is_race_free_for_every_size():
 
 
 def test_step_group_plan_merges_what_fits():
-    """mrts_step_group_plan (host logic, no workspace needed): configs[4]'s buckets -- 8x8,
-    16x16 and 24x24 (40 KB fused workgroups since round 4: four per CU) share a launch
-    under merge-fit, a 32x32 bucket (70 KB) keeps its own; merge-all puts all in one;
-    separate gives one each; engines of other planes or bot fusion never share; a handle
-    listed twice is rejected."""
+    """mrts_step_group_plan (host logic, no workspace needed): configs[4]'s buckets -- 8x8
+    and 16x16 share a launch under merge-fit (members that keep >= 6 workgroups per CU),
+    24x24 (40 KB fused workgroups: four per CU) and 32x32 keep their own; merge-all puts
+    all in one; separate gives one each; engines of other planes or bot fusion never share;
+    a handle listed twice is rejected."""
     from gym_microrts import _native
 
     lib = _native.lib()
@@ -157,7 +157,7 @@ def test_step_group_plan_merges_what_fits():
 
     h8, h16, h24 = mk("maps/8x8/basesWorkers8x8.xml"), mk("maps/16x16/basesWorkers16x16.xml"), mk("maps/24x24/basesWorkers24x24.xml")
     hs = [h8, h16, h24]
-    assert plan(hs, _native.GROUP_MERGE_FIT | _native.GROUP_BOTS_FIRST) == (0, [0, 0, 0], 1)
+    assert plan(hs, _native.GROUP_MERGE_FIT | _native.GROUP_BOTS_FIRST) == (0, [0, 0, 1], 2)
     h32 = mk("maps/32x32/basesWorkers32x32.xml")
     assert plan([h8, h16, h32], _native.GROUP_MERGE_FIT) == (0, [0, 0, 1], 2)
     assert plan([h8, h16, h32], _native.GROUP_MERGE_ALL) == (0, [0, 0, 0], 1)

@@ -214,9 +214,9 @@ def test_mixed_map_buckets_match_oracle(concurrent, group_policy):
             ("maps/24x24/basesWorkers24x24.xml", 4, ["workerRushAI", "coacAI"])]
     env = mixed_lockstep(spec, 400, concurrent=concurrent, group_policy=group_policy)
     assert env.grouped == (group_policy is not None)
-    # the launches (mrts_step_group_plan): since round 4 the 24x24 bucket's fused workgroups
-    # take 40 KB (four per CU), so merge-fit puts all three buckets in one launch
-    expect = {None: ([0, 1, 2], 3), 0: ([0, 1, 2], 3), 5: ([0, 0, 0], 1), 2: ([0, 0, 0], 1), 6: ([0, 0, 0], 1)}
+    # the launches (mrts_step_group_plan): merge-fit merges what keeps >= 6 workgroups per CU
+    # (the step kernel's own occupancy), so the 24x24 bucket's 40 KB workgroups keep their own
+    expect = {None: ([0, 1, 2], 3), 0: ([0, 1, 2], 3), 5: ([0, 0, 1], 2), 2: ([0, 0, 0], 1), 6: ([0, 0, 0], 1)}
     assert env.launch_plan() == expect[group_policy]
 
 
