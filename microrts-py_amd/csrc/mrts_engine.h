@@ -15,13 +15,19 @@
 static __device__ unsigned long long g_stamp[MRTS_STAMP_ROWS][MRTS_STAMP_COLS];
 static __device__ unsigned int g_stamp_n;
 __shared__ int mrts_stamp_row;
+// mrts_stamp_row: set by k_step's thread 0 before a barrier; every other kernel
+// that reaches a stamp site (k_reset / k_masks through emit_outputs) sets it to -1
+// first (MRTS_STAMP_NONE), and the unsigned bound check skips it
 #define MRTS_STAMP(k, cond) \
-    do { if ((cond) && mrts_stamp_row < MRTS_STAMP_ROWS) g_stamp[mrts_stamp_row][k] = wall_clock64(); } while (0)
+    do { if ((cond) && (unsigned)mrts_stamp_row < (unsigned)MRTS_STAMP_ROWS) g_stamp[mrts_stamp_row][k] = wall_clock64(); } while (0)
 #define MRTS_STAMP_MAX(k, cond) \
-    do { if ((cond) && mrts_stamp_row < MRTS_STAMP_ROWS) atomicMax(&g_stamp[mrts_stamp_row][k], (unsigned long long)wall_clock64()); } while (0)
+    do { if ((cond) && (unsigned)mrts_stamp_row < (unsigned)MRTS_STAMP_ROWS) \
+             atomicMax(&g_stamp[mrts_stamp_row][k], (unsigned long long)wall_clock64()); } while (0)
+#define MRTS_STAMP_NONE() do { if (threadIdx.x == 0) mrts_stamp_row = -1; __syncthreads(); } while (0)
 #else
 #define MRTS_STAMP(k, cond) do { } while (0)
 #define MRTS_STAMP_MAX(k, cond) do { } while (0)
+#define MRTS_STAMP_NONE() do { } while (0)
 #endif
 
 struct EngineParams {

@@ -519,6 +519,7 @@ __device__ __forceinline__ void zero_outputs(const EngineParams& p, const Game& 
 template <int NT, int P, typename OT>
 __global__ __launch_bounds__(NT) void k_reset(EngineParams p, const int32_t* games, const int32_t* maps, int count) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    MRTS_STAMP_NONE();
     Lds L = carve(smem, p.HW, p.W, NT);
     int g = games ? games[blockIdx.x] : blockIdx.x;
     if (game_parked(p, g)) {
@@ -581,6 +582,7 @@ __global__ __launch_bounds__(NT) void k_raw(EngineParams p, int32_t* raw) {
 template <int NT>
 __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    MRTS_STAMP_NONE();
     Lds L = carve(smem, p.HW, p.W, NT);
     const int g = blockIdx.x;
     if (game_parked(p, g)) {   // the caller's buffers need not be the ones zeroed at park time
@@ -980,6 +982,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     if (game_parked(p, g)) return;   // no tick: its outputs stay zero (mrts_park_games)
     if (pf_ok) prefetch_game<NT, FB>(p, g, pf);
     else if (pf_wide) prefetch_wide<NT>(p, game_of(p, g), g, wpf);
+    MRTS_STAMP(15, threadIdx.x == 0);
     if (FB && P == 29 && p.early_bot && g >= p.nsp_games && NT > 64) {   // the early bot's tail arrays start zeroed
         uint32_t* t = reinterpret_cast<uint32_t*>(smem + fb_tail_offset(HW, p.W, NT, true));
         for (int i = threadIdx.x; i < (int)(bots::bot_tail_bytes(HW, p.W) / 4); i += NT) t[i] = 0;

@@ -54,7 +54,9 @@ def main():
     envs, one_step = build(args, dev)
     for e in envs:
         e.reset()
+    print(f"stamps_run: {a.workload} {a.envs_per_gpu} envs, pre-roll ...", flush=True)
     s0 = bench.preroll(envs, one_step, args.max_steps if args.preroll < 0 else args.preroll)
+    print(f"stamps_run: pre-roll done ({s0} ticks)", flush=True)
     for s in range(s0, s0 + 10):
         one_step(s)
     torch.cuda.synchronize()
@@ -113,13 +115,14 @@ def build(args, dev):
     return [env], one_step
 
 
-PHASES = [("commit", 2, 3), ("decode", 3, 4), ("issue", 4, 5), ("cycle", 5, 6), ("tail", 6, 7)]
+PHASES = [("pf_issue", 2, 15), ("pf_wait", 15, 3), ("commit", 2, 3), ("decode", 3, 4), ("issue", 4, 5), ("cycle", 5, 6), ("tail", 6, 7)]
 
 
 def report(steps, a):
     out = {"workload": a.workload, "envs": a.envs_per_gpu, "steps": len(steps), "groups": {}}
     acc = {}
     for r in steps:
+        r = r[r[:, 2] > 0]   # rows of workgroups that ran this step
         hw = (r[:, 0] >> np.uint64(32)).astype(np.int64)
         kind = r[:, 1].astype(np.int64)
         t = r.astype(np.float64)
@@ -133,6 +136,10 @@ def report(steps, a):
                 m = sel & (hw == key[0]) & ((kind & 1) == key[1])
                 g = acc.setdefault(f"{int(key[0])}{'_bot' if key[1] else '_selfplay'}", {})
                 tt = t[m]
+                first = (tt[:, 2] - t0) * TICK_US < 2.0
+                ok = (tt[:, 3] > 0)
+                g.setdefault("commit_first_round", []).extend((tt[first & ok, 3] - tt[first & ok, 2]) * TICK_US)
+                g.setdefault("commit_later", []).extend((tt[~first & ok, 3] - tt[~first & ok, 2]) * TICK_US)
                 def d(i, j):
                     ok = (tt[:, i] > 0) & (tt[:, j] > 0)
                     return (tt[ok, j] - tt[ok, i]) * TICK_US
