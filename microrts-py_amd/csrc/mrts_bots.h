@@ -1253,7 +1253,7 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     // (mrts_engine.hip bot_setup_workgroup) and zeroed the tail arrays
     for (int c = lane; !preset && c < HW; c += BT) {
         if (!FUSED) {
-            int4 v = p.cells[(size_t)g * HW + c];
+            int4 v = p.cells[(size_t)g * p.cstride + c];
             L.unit[c] = (uint32_t)v.x;
             L.uid[c] = v.y;
             L.act[c] = (uint32_t)v.z;

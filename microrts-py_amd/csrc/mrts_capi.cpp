@@ -149,6 +149,13 @@ std::string utt_json() {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// int4 records between consecutive games' cell rows: HW plus MRTS_CELL_PAD (A/B
+// experiments on the HBM placement of the per-game rows)
+#ifndef MRTS_CELL_PAD
+#define MRTS_CELL_PAD 0
+#endif
+int cell_stride(int HW) { return HW + MRTS_CELL_PAD; }
+
 }  // namespace
 
 struct mrts_vec {
@@ -259,7 +266,7 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
             return fail(h, MRTS_ENOTIMPL, "map too large for the bot kernel's LDS");
     }
     size_t o = 0;
-    h->off_cells = o; o = align256(o + (size_t)h->ngames * h->HW * sizeof(int4));
+    h->off_cells = o; o = align256(o + (size_t)h->ngames * cell_stride(h->HW) * sizeof(int4));
     h->off_genv = o; o = align256(o + (size_t)h->ngames * MRTS_GENV_WORDS * sizeof(int32_t));
     h->off_mcells = o; o = align256(o + (size_t)h->map_capacity * h->HW * sizeof(int4));
     h->off_mwall = o; o = align256(o + (size_t)h->map_capacity * h->HW);
@@ -319,6 +326,7 @@ int mrts_bind_workspace(mrts_vec *h, void *dev, void *stream) {
     EngineParams &p = h->base;
     p = EngineParams{};
     p.cells = (int4 *)(h->ws + h->off_cells);
+    p.cstride = cell_stride(h->HW);
     p.genv = (int32_t *)(h->ws + h->off_genv);
     p.map_cells = (const int4 *)(h->ws + h->off_mcells);
     p.map_wall = (const uint8_t *)(h->ws + h->off_mwall);

@@ -13,7 +13,6 @@
 #define MRTS_STAMP_ROWS 65536
 #define MRTS_STAMP_COLS 16
 static __device__ unsigned long long g_stamp[MRTS_STAMP_ROWS][MRTS_STAMP_COLS];
-static __device__ unsigned int g_stamp_n;
 __shared__ int mrts_stamp_row;
 // mrts_stamp_row: set by k_step's thread 0 before a barrier; every other kernel
 // that reaches a stamp site (k_reset / k_masks through emit_outputs) sets it to -1
@@ -31,7 +30,8 @@ __shared__ int mrts_stamp_row;
 #endif
 
 struct EngineParams {
-    int4 *cells;            // [G][HW]
+    int4 *cells;            // [G][cstride] (the first HW records of each game's row)
+    int cstride;            // int4 records between consecutive games' cells (>= HW)
     int32_t *genv;          // [G][MRTS_GENV_WORDS]
     const int4 *map_cells;  // [maps][HW]
     const uint8_t *map_wall;// [maps][HW]

@@ -331,7 +331,7 @@ __device__ __forceinline__ void load_game(const EngineParams& p, const Lds& L, i
     if (threadIdx.x < MRTS_GENV_WORDS) L.sc[threadIdx.x] = p.genv[(size_t)g * MRTS_GENV_WORDS + threadIdx.x];
     __syncthreads();
     const int HW = p.HW, map = L.sc[SC_MAP];
-    const int4* src = p.cells + (size_t)g * HW;
+    const int4* src = p.cells + (size_t)g * p.cstride;
     for (int c = threadIdx.x; c < HW; c += NT) {
         int4 v = src[c];
         L.unit[c] = (uint32_t)v.x;
@@ -346,7 +346,7 @@ __device__ __forceinline__ void load_game(const EngineParams& p, const Lds& L, i
 template <int NT>
 __device__ __forceinline__ void store_game(const EngineParams& p, const Lds& L, int g) {
     const int HW = p.HW;
-    int4* dst = p.cells + (size_t)g * HW;
+    int4* dst = p.cells + (size_t)g * p.cstride;
     for (int c = threadIdx.x; c < HW; c += NT) dst[c] = make_int4((int)L.unit[c], L.uid[c], (int)L.act[c], (int)L.seq[c]);
     if (threadIdx.x < MRTS_GENV_WORDS) p.genv[(size_t)g * MRTS_GENV_WORDS + threadIdx.x] = L.sc[threadIdx.x];
 }
@@ -859,7 +859,7 @@ __device__ __forceinline__ void prefetch_wide(const EngineParams& p, const Game&
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int c = min((int)threadIdx.x + k * NT, HW - 1);   // unconditional: counted waits
-        pf.cell[k] = p.cells[(size_t)g * HW + c];
+        pf.cell[k] = p.cells[(size_t)g * p.cstride + c];
         const int s0 = p.src[(size_t)G.env0 * HW + c], s1 = p.src[(size_t)(G.env0 + G.nviews - 1) * HW + c];
         pf.src[k] = (s0 ? 1 : 0) | (s1 ? 2 : 0);
         if (p.nmaps == 1) pf.wall[k] = p.map_wall[c];
@@ -900,11 +900,17 @@ struct StatePf {
     int wall;         // single-map batches: this cell's terrain
     int map;          // the game's map (genv[MRTS_G_MAP], every lane: no barrier before the terrain load)
 };
+// the bot wave's first abstract-action words: lane, lane + 64 of the game's 2 * HW (clamped: small maps)
+__device__ __forceinline__ void prefetch_aa(const EngineParams& p, int g, StatePf& pf) {
+    const int4* aa = p.aa + ((size_t)(g - p.nsp_games) * 2 + 1) * p.HW * 2;
+    pf.aa = aa[min((int)threadIdx.x, 2 * p.HW - 1)];
+    pf.aa2 = aa[min(64 + (int)threadIdx.x, 2 * p.HW - 1)];
+}
 template <int NT, bool FB>
 __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, StatePf& pf) {
     const Game G = game_of(p, g);
     const int HW = p.HW, c = min((int)threadIdx.x, HW - 1);   // unconditional: counted waits
-    pf.cell = p.cells[(size_t)g * HW + c];
+    pf.cell = p.cells[(size_t)g * p.cstride + c];
     pf.src0 = p.src[(size_t)G.env0 * HW + c];
     pf.src1 = p.src[(size_t)(G.env0 + G.nviews - 1) * HW + c];
     pf.genv = p.genv[(size_t)g * MRTS_GENV_WORDS + min((int)threadIdx.x, MRTS_GENV_WORDS - 1)];
@@ -912,11 +918,9 @@ __device__ __forceinline__ void prefetch_game(const EngineParams& p, int g, Stat
         const int32_t* bp = p.botpa + (size_t)(g - p.nsp_games) * 2 * HW;
         pf.bpa0 = p.bot_ai0 ? bp[c] : 0;   // player 0 bots: MicroRTSBotVecEnv only
         pf.bpa1 = bp[HW + c];
-        if (FB && threadIdx.x < 64) {   // words lane, lane + 64 of the game's 2 * HW (clamped: small maps)
-            const int4* aa = p.aa + ((size_t)(g - p.nsp_games) * 2 + 1) * HW * 2;
-            pf.aa = aa[min((int)threadIdx.x, 2 * HW - 1)];
-            pf.aa2 = aa[min(64 + (int)threadIdx.x, 2 * HW - 1)];
-        }
+#ifndef MRTS_DEFER_AA
+        if (FB && threadIdx.x < 64) prefetch_aa(p, g, pf);
+#endif
     }
     if (p.nmaps == 1) pf.wall = p.map_wall[c];   // else the game's map is known only with genv
     else pf.map = p.genv[(size_t)g * MRTS_GENV_WORDS + MRTS_G_MAP];
@@ -963,8 +967,9 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
 #ifdef MRTS_STAMPS
     if (threadIdx.x == 0) {   // rows by workgroup (no atomics: they would skew the start stamps);
         // maps of more than 256 cells launch apart from the others (mrts_step_group plans)
+        // (no row counter: an atomic on one address by every workgroup sits in the vmcnt
+        // queue ahead of the state loads and skewed the first round by ~10 us)
         mrts_stamp_row = (int)blockIdx.x + (HW > 256 ? MRTS_STAMP_ROWS / 2 : 0);
-        atomicMax(&g_stamp_n, (unsigned)mrts_stamp_row + 1u);
         if (mrts_stamp_row < MRTS_STAMP_ROWS) {
             g_stamp[mrts_stamp_row][0] = (unsigned long long)g | ((unsigned long long)HW << 32);
             g_stamp[mrts_stamp_row][1] = (unsigned long long)(g >= p.nsp_games) | ((unsigned long long)(FB && NT > 64) << 1) |
@@ -1006,6 +1011,9 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     }
     if (pf_ok) {
         commit_game<NT>(p, L, pf);
+#ifdef MRTS_DEFER_AA
+        if (FB && !G.selfplay && p.botpa && threadIdx.x < 64) prefetch_aa(p, g, pf);   // after the state's round trip
+#endif
     } else if (pf_wide) {
         commit_wide<NT>(p, L, wpf);
     } else {
@@ -1765,13 +1773,11 @@ static hipError_t step_group(const EngineParams* ps, int n, hipStream_t s, bool 
 
 extern "C" {
 #ifdef MRTS_STAMPS
-// experiment builds: copy the stamp rows of the launches since the last reset
-// (reset != 0 zeroes the rows and the row counter first); returns the row count
+// experiment builds: copy the stamp rows (every row; rows of workgroups that did not
+// run since the last reset are zero) and, with reset != 0, zero them afterwards;
+// returns the row count copied
 int mrts_debug_stamps(unsigned long long* out, int max_rows, int reset) {
-    unsigned int n = 0;
-    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_stamp_n), sizeof n, 0, hipMemcpyDeviceToHost)) return -1;
-    n = n < (unsigned)MRTS_STAMP_ROWS ? n : (unsigned)MRTS_STAMP_ROWS;
-    const int rows = (int)n < max_rows ? (int)n : max_rows;
+    const int rows = MRTS_STAMP_ROWS < max_rows ? MRTS_STAMP_ROWS : max_rows;
     if (out && rows > 0 &&
         hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * MRTS_STAMP_COLS * rows, 0, hipMemcpyDeviceToHost))
         return -1;
@@ -1779,8 +1785,6 @@ int mrts_debug_stamps(unsigned long long* out, int max_rows, int reset) {
         static unsigned long long zero[1024][MRTS_STAMP_COLS];
         for (int r = 0; r < MRTS_STAMP_ROWS; r += 1024)
             if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), zero, sizeof zero, sizeof zero * (r / 1024), hipMemcpyHostToDevice)) return -1;
-        const unsigned int z = 0;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_n), &z, sizeof z, 0, hipMemcpyHostToDevice)) return -1;
     }
     return rows;
 }
@@ -1824,7 +1828,7 @@ hipError_t mrts_engine_sample_src(const int32_t* mask, const int32_t* src, int n
 }
 hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, int map, int size, uint8_t* rgb) {
     const int nblk = (size * size + 255) / 256;
-    hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->HW, p->map_wall + (size_t)map * p->HW,
+    hipLaunchKernelGGL(mrts::k_render, dim3(nblk), dim3(256), 0, s, p->cells + (size_t)game * p->cstride, p->map_wall + (size_t)map * p->HW,
                        p->W, p->H, size, rgb);
     return hipGetLastError();
 }

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r04j; mkdir -p $O
+for spec in "coac 1024" "selfplay 8192" "selfplay 1024"; do
+  set -- $spec
+  timeout -k 10 240 python -u scripts/stamps_run.py --workload $1 --envs-per-gpu $2 --steps 6 --dump $O/raw_$1_$2.npz > $O/st_$1_$2.txt 2>&1
+done

@@ -36,6 +36,11 @@ def main():
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--lib", default=os.path.join(REPO, "scripts", "ab", "libs", "stamps.so"))
     ap.add_argument("--json", default=None)
+    ap.add_argument("--dump", default=None, help="np.save the raw stamp rows of every measured step (a list) here")
+    ap.add_argument("--gap-us", type=float, default=0.0,
+                    help="idle time between the sampler and the step of each measured step (synchronize + sleep)")
+    ap.add_argument("--read-mb", type=int, default=0,
+                    help="read a clean buffer of this size between the sampler and the step (evicts dirty cache lines)")
     a = ap.parse_args()
     from gym_microrts import _native
 
@@ -51,7 +56,8 @@ def main():
                         "--preroll", str(a.preroll), "--no-kernel-events"])
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    envs, one_step = build(args, dev)
+    gap = [0.0]
+    envs, one_step = build(args, dev, gap)
     for e in envs:
         e.reset()
     print(f"stamps_run: {a.workload} {a.envs_per_gpu} envs, pre-roll ...", flush=True)
@@ -62,17 +68,38 @@ def main():
     torch.cuda.synchronize()
     rows = []
     buf = np.zeros((65536, 16), np.uint64)
+    gap[0] = a.gap_us * 1e-6
+    if a.read_mb:
+        gap.append(torch.ones(a.read_mb << 18, dtype=torch.float32, device=dev))
     for k in range(a.steps):
-        L.mrts_debug_stamps(None, 0, 1)
+        L.mrts_debug_stamps(None, 0, 1)   # zero the rows
         one_step(s0 + 10 + k)
         torch.cuda.synchronize()
         n = L.mrts_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.shape[0], 0)
         assert n > 0, "no stamps: is this the STAMPS=1 library?"
         rows.append(buf[:n].copy())
+    if a.dump:
+        np.savez_compressed(a.dump, *rows)
     report(rows, a)
 
 
-def build(args, dev):
+def _gap(gap):
+    if len(gap) > 1:
+        import torch
+
+        torch.cuda.synchronize()
+        gap[1].sum()
+        torch.cuda.synchronize()
+    if gap[0] > 0:
+        import time
+
+        import torch
+
+        torch.cuda.synchronize()
+        time.sleep(gap[0])
+
+
+def build(args, dev, gap):
     """The bench's env + loop (bench.run_gpu / run_mixed) without its timing."""
     import numpy as np
     import torch
@@ -97,6 +124,7 @@ def build(args, dev):
             masks = env.get_action_mask()
             for e, m, ac in zip(env.envs, masks, acts):
                 _native.check(bench.sample(lib, "src", m, e.source_unit_mask, e.num_envs, e.height * e.width, 0, 1, s, ac))
+            _gap(gap)
             return env.step(acts)
         return env.envs, one_step
     wmap, nsp, nbot, bot, po = bench.WORKLOADS[args.workload]
@@ -111,6 +139,7 @@ def build(args, dev):
     def one_step(s):
         env.get_action_mask()
         _native.check(bench.sample(lib, "src", env._mask, env._src, n, hw, 0, 1, s, act))
+        _gap(gap)
         return env.step(act)
     return [env], one_step
 
