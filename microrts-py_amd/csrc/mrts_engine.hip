@@ -447,14 +447,25 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             // the last store of the run ends at plane P-1.)  A one-hot word has no
             // bit at or above P, so (w0 >> pl) | (w1 << (P - pl)) are the window's
             // bits.  (c, pl) advance by a constant per trip: no division in the loop.
-            const int dq = 4 * nt / P, dr = 4 * nt - dq * P;
+            // Software-pipelined: the next trip's word pair is read before this trip's
+            // store, so the LDS round trip overlaps the bit work instead of stalling every
+            // trip (a lone workgroup's stream -- the kernel's last round -- is bound by this
+            // loop, not by the store path: scripts/store_rate.hip).  The read-ahead index is
+            // clamped into the word region (its last trip's values are never used).
+            const int dq = 4 * nt / P, dr = 4 * nt - dq * P, cmax = NV * HW - 1;
             int c = 4 * t0 / P, pl = 4 * t0 - c * P;
+            uint32_t w0 = ow[min(c, cmax)], w1 = ow[min(c, cmax) + 1];
             for (int k = t0; k < total / 4; k += nt) {
-                const uint32_t bits = (ow[c] >> pl) | (ow[c + 1] << (P - pl));
+                int cn = c + dq, pn = pl + dr;
+                if (pn >= P) { pn -= P; cn++; }
+                const int cr = min(cn, cmax);
+                const uint32_t n0 = ow[cr], n1 = ow[cr + 1];
+                const uint32_t bits = (w0 >> pl) | (w1 << (P - pl));
                 st16(out + 4 * k, (bits & 1u) ? ONE : 0, (bits & 2u) ? ONE : 0, (bits & 4u) ? ONE : 0, (bits & 8u) ? ONE : 0);
-                c += dq;
-                pl += dr;
-                if (pl >= P) { pl -= P; c++; }
+                w0 = n0;
+                w1 = n1;
+                c = cn;
+                pl = pn;
             }
         } else {
             for (int e = t0; e < total; e += nt) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
@@ -472,18 +483,25 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             // (r, ch) advance by a constant per trip; the ch == 76 fix-up is a select,
             // not a branch.
             static_assert(MRTS_MASK_CH == 78, "mask row layout");
-            const int dq = 4 * nt / MRTS_MASK_CH, dr = 4 * nt - dq * MRTS_MASK_CH;
+            // (software-pipelined as the obs loop: the next trip's word pair read ahead)
+            const int dq = 4 * nt / MRTS_MASK_CH, dr = 4 * nt - dq * MRTS_MASK_CH, wmax = 3 * NV * HW - 1;
             int r = 4 * t0 / MRTS_MASK_CH, ch = 4 * t0 - r * MRTS_MASK_CH;
             int r3 = 3 * r;   // the row's first word
+            int wr = min(r3 + ((ch + 1) >> 5), wmax);
+            uint32_t lo = mw[wr], hi = mw[wr + 1];
             for (int k = t0; k < total / 4; k += nt) {
-                const int b0 = ch + 1, w = r3 + (b0 >> 5);
-                const uint32_t lo = mw[w], hi = mw[w + 1];
+                int r3n = r3 + 3 * dq, chn = ch + dr;
+                if (chn >= MRTS_MASK_CH) { chn -= MRTS_MASK_CH; r3n += 3; }
+                wr = min(r3n + ((chn + 1) >> 5), wmax);
+                const uint32_t nlo = mw[wr], nhi = mw[wr + 1];
+                const int b0 = ch + 1;
                 const uint32_t fun = (uint32_t)((((uint64_t)hi << 32) | lo) >> (b0 & 31));
                 const uint32_t bits = ch == 76 ? ((fun & 3u) | ((hi << 1) & 0xCu)) : fun;
                 st16(out + 4 * k, (int)(bits & 1u), (int)((bits >> 1) & 1u), (int)((bits >> 2) & 1u), (int)((bits >> 3) & 1u));
-                r3 += 3 * dq;
-                ch += dr;
-                if (ch >= MRTS_MASK_CH) { ch -= MRTS_MASK_CH; r3 += 3; }
+                lo = nlo;
+                hi = nhi;
+                r3 = r3n;
+                ch = chn;
             }
         } else {
             for (int e = t0; e < total; e += nt) {
@@ -1032,9 +1050,10 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     //   a pending produce is over its owner's budget; + the target positions the
     //   agent's move / produce rows claim (step 2a)
     int units = 0;   // player 0's units + player 1's << 16 (SC_HAS)
-    for (int c = threadIdx.x; c < HW; c += NT) {
-        uint32_t u = L.unit[c], nw = 0;
-        int ow = u_owner(u);
+    // per cell: unit counts, pending reservations / produce budgets; returns the
+    // view whose agent row the cell's idle unit may take (-1: none)
+    auto cell_pass = [&](int c, uint32_t u) {
+        const int ow = u_owner(u);
         if (u != 0 && (ow == 0 || ow == 1)) units += ow ? 1 << 16 : 1;
         const uint32_t pa = L.act[c];
         if (pa) {
@@ -1049,38 +1068,69 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                 }
             }
         }
-        if (u != 0 && ow >= 0 && pa == 0) {
-            int view = G.selfplay ? ow : (ow == 0 && !bot0 ? 0 : -1);
-            if (view >= 0) {
-                const size_t row = (size_t)(G.env0 + view) * HW + c;
-                if (pf_wide ? (L.aux[c] >> view) & 1u : c == (int)threadIdx.x ? src_pre[view] : p.src[row]) {
-                    const int64_t* ra = p.actions + row * 7;
-                    int64_t r[7];   // all 7 components in one round trip
+        return (u != 0 && ow >= 0 && pa == 0) ? (G.selfplay ? ow : (ow == 0 && !bot0 ? 0 : -1)) : -1;
+    };
+    // the agent's action row of cell c's idle unit (view v, owner ow): decode +
+    // legality + the target claims; returns its aux word
+    auto decode_row = [&](int c, int v, int ow) -> uint32_t {
+        const int64_t* ra = p.actions + ((size_t)(G.env0 + v) * HW + c) * 7;
+        int64_t r[7];   // all 7 components in one round trip
 #pragma unroll
-                    for (int k = 0; k < 7; k++) r[k] = ra[k];
-                    int64_t ty = r[0];
-                    int code = -1;
-                    if (ty == A_NONE) code = code_make(A_NONE, 1, 0);   // NONE(1): param = duration
-                    else if (ty >= A_MOVE && ty <= A_RETURN) {
-                        int64_t d = r[ty];
-                        if (d >= 0 && d < 4) code = code_make((int)ty, (int)d, 0);
-                    } else if (ty == A_PRODUCE) {
-                        int64_t d = r[4], t2 = r[5];
-                        if (d >= 0 && d < 4 && t2 >= 0 && t2 < MRTS_NTYPES) code = code_make(A_PRODUCE, (int)d, (int)t2);
-                    } else if (ty == A_ATTACK) {
-                        int64_t a = r[6];
-                        if (a >= 0 && a < MRTS_ATTACK_GRID * MRTS_ATTACK_GRID) code = code_make(A_ATTACK, (int)a, 0);
-                    }
-                    if (code >= 0) {
-                        bool lg = legal_code(gd, c, code, L.unit, L.wall, res_of(L, ow));
-                        nw = CAND | (lg ? LEGAL : 0u) | (uint32_t)code;
-                        claim_target(L, gd, c, code, posw);
-                        if (code_type(code) == A_PRODUCE) atomicAdd(&L.sc[SC_PSUM + ow], ut_cost(code_utype(code)));
-                    }
-                }
-            }
+        for (int k = 0; k < 7; k++) r[k] = ra[k];
+        int64_t ty = r[0];
+        int code = -1;
+        if (ty == A_NONE) code = code_make(A_NONE, 1, 0);   // NONE(1): param = duration
+        else if (ty >= A_MOVE && ty <= A_RETURN) {
+            int64_t d = r[ty];
+            if (d >= 0 && d < 4) code = code_make((int)ty, (int)d, 0);
+        } else if (ty == A_PRODUCE) {
+            int64_t d = r[4], t2 = r[5];
+            if (d >= 0 && d < 4 && t2 >= 0 && t2 < MRTS_NTYPES) code = code_make(A_PRODUCE, (int)d, (int)t2);
+        } else if (ty == A_ATTACK) {
+            int64_t a = r[6];
+            if (a >= 0 && a < MRTS_ATTACK_GRID * MRTS_ATTACK_GRID) code = code_make(A_ATTACK, (int)a, 0);
         }
-        L.aux[c] = nw;
+        if (code < 0) return 0u;
+        const bool lg = legal_code(gd, c, code, L.unit, L.wall, res_of(L, ow));
+        claim_target(L, gd, c, code, posw);
+        if (code_type(code) == A_PRODUCE) atomicAdd(&L.sc[SC_PSUM + ow], ut_cost(code_utype(code)));
+        return CAND | (lg ? LEGAL : 0u) | (uint32_t)code;
+    };
+    if (!pf_wide) {   // one cell per lane (maps of <= NT cells) or the unprefetched path
+        for (int c = threadIdx.x; c < HW; c += NT) {
+            const uint32_t u = L.unit[c];
+            const int v = cell_pass(c, u);
+            uint32_t nw = 0;
+            if (v >= 0 && (c == (int)threadIdx.x ? src_pre[v] : p.src[(size_t)(G.env0 + v) * HW + c])) nw = decode_row(c, v, u_owner(u));
+            L.aux[c] = nw;
+        }
+    } else {
+        // wider maps: the rows to decode are gathered per wave first (ballots; the
+        // source words came with the prefetch, in aux) and then loaded one per lane,
+        // so the lane's two to four cells cost one action-row round trip, not one each.
+        // The wave's list lives in L.list / L.prod (2 HW words, used later only by the
+        // compactions): wave w takes [w K 64, (w + 1) K 64), K = cells per lane <= 4.
+        const int K = (HW + NT - 1) / NT, lane = threadIdx.x & 63;
+        int32_t* const wl = L.list + (threadIdx.x >> 6) * K * 64;
+        int wn = 0;
+        for (int k = 0; k < K; k++) {   // uniform trip count: every lane takes part in each ballot
+            const int c = (int)threadIdx.x + k * NT;
+            int e = -1;
+            if (c < HW) {
+                const uint32_t u = L.unit[c];
+                const int v = cell_pass(c, u);
+                if (v >= 0 && ((L.aux[c] >> v) & 1u)) e = c | (v << 16);
+                L.aux[c] = 0;
+            }
+            const unsigned long long m = __ballot(e >= 0);
+            if (e >= 0) wl[wn + __popcll(m & ((1ull << lane) - 1ull))] = e;
+            wn += __popcll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        for (int j = lane; j < wn; j += 64) {
+            const int e = wl[j], c = e & 0xFFFF, v = e >> 16;
+            L.aux[c] = decode_row(c, v, u_owner(L.unit[c]));
+        }
     }
     if (units) atomicAdd(&L.sc[SC_HAS], units);
     // the device bot's PlayerAction for player 1 (k_bot, computed on the state
