@@ -238,6 +238,19 @@ int mrts_game_stats(mrts_vec *h, void *stream, int32_t *out);
  * Drawing rules: DESIGN.md §4c (the Java panel is absent; parity unpinned). */
 int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t size);
 
+/* Env-state checkpoint (no reference counterpart; SURVEY.md §5 "env-state
+ * checkpoint"): the games' whole state -- cells, scalars, map templates, the
+ * device bots' abstract actions and PlayerActions, parked flags, and the host-side
+ * mirrors -- copied into / out of a caller device buffer of mrts_state_bytes(h)
+ * bytes (256-byte aligned).  mrts_save_state synchronises the stream.
+ * mrts_load_state restores a snapshot of the same configuration and map table
+ * into this handle (MRTS_EINVAL otherwise) and writes the restored state's obs
+ * into `obs` (and its next-tick masks into the bound mask outputs), as mrts_reset
+ * does for a fresh state; stepping on from it repeats the saved run bit for bit. */
+size_t mrts_state_bytes(const mrts_vec *h);
+int mrts_save_state(mrts_vec *h, void *stream, void *dst);
+int mrts_load_state(mrts_vec *h, void *stream, const void *src, void *obs);
+
 /* Engine invariant violations recorded on the device (OR over games). */
 int mrts_error_flags(mrts_vec *h, void *stream, int32_t *flags_out);
 

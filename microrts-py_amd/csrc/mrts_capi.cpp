@@ -728,6 +728,67 @@ int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t si
     return e ? hip_fail(h, e, "render launch") : MRTS_OK;
 }
 
+// Env-state checkpoint: [header | workspace bytes].  The header carries what the
+// host holds beside the workspace (bots_ready, the games' map indices, parked flags)
+// and the shape the snapshot belongs to.
+namespace {
+struct StateHeader {
+    uint32_t magic, version;
+    int32_t ngames, HW, nmaps, bots_ready, parked_any;
+    uint64_t total;
+};
+const uint32_t kStateMagic = 0x4d525453u;   // "MRTS"
+size_t state_header_bytes(const mrts_vec *h) {
+    return align256(sizeof(StateHeader) + (size_t)h->ngames * (sizeof(int32_t) + 1));
+}
+}  // namespace
+
+size_t mrts_state_bytes(const mrts_vec *h) { return bound(const_cast<mrts_vec *>(h)) ? state_header_bytes(h) + h->total : 0; }
+
+int mrts_save_state(mrts_vec *h, void *stream, void *dst) {
+    if (!bound(h) || !dst) return fail(h, MRTS_ESTATE, "save_state: workspace not bound or dst null");
+    if (((uintptr_t)dst & 255u) != 0) return fail(h, MRTS_EINVAL, "save_state: dst must be 256-byte aligned");
+    std::vector<unsigned char> hdr(state_header_bytes(h), 0);
+    StateHeader sh{kStateMagic, 1, h->ngames, h->HW, (int32_t)h->maps.size(), h->bots_ready ? 1 : 0,
+                   h->base.parked != nullptr ? 1 : 0, (uint64_t)h->total};
+    std::memcpy(hdr.data(), &sh, sizeof sh);
+    std::memcpy(hdr.data() + sizeof sh, h->game_map.data(), (size_t)h->ngames * sizeof(int32_t));
+    std::memcpy(hdr.data() + sizeof sh + (size_t)h->ngames * sizeof(int32_t), h->parked.data(), (size_t)h->ngames);
+    hipStream_t s = (hipStream_t)stream;
+    unsigned char *d = (unsigned char *)dst;
+    hipError_t e = hipMemcpyAsync(d, hdr.data(), hdr.size(), hipMemcpyHostToDevice, s);
+    if (!e) e = hipMemcpyAsync(d + hdr.size(), h->ws, h->total, hipMemcpyDeviceToDevice, s);
+    if (!e) e = hipStreamSynchronize(s);   // the host header buffer is this call's
+    return e ? hip_fail(h, e, "save_state copy") : MRTS_OK;
+}
+
+int mrts_load_state(mrts_vec *h, void *stream, const void *src, void *obs) {
+    if (!bound(h) || !src || !obs) return fail(h, MRTS_ESTATE, "load_state: workspace not bound or null buffer");
+    if (((uintptr_t)src & 255u) != 0) return fail(h, MRTS_EINVAL, "load_state: src must be 256-byte aligned");
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<unsigned char> hdr(state_header_bytes(h), 0);
+    hipError_t e = hipMemcpyAsync(hdr.data(), src, hdr.size(), hipMemcpyDeviceToHost, s);
+    if (!e) e = hipStreamSynchronize(s);
+    if (e) return hip_fail(h, e, "load_state header");
+    StateHeader sh;
+    std::memcpy(&sh, hdr.data(), sizeof sh);
+    if (sh.magic != kStateMagic || sh.version != 1 || sh.ngames != h->ngames || sh.HW != h->HW || sh.nmaps != (int32_t)h->maps.size() ||
+        sh.total != (uint64_t)h->total)
+        return fail(h, MRTS_EINVAL, "load_state: the snapshot belongs to another configuration or map table");
+    std::memcpy(h->game_map.data(), hdr.data() + sizeof sh, (size_t)h->ngames * sizeof(int32_t));
+    std::memcpy(h->parked.data(), hdr.data() + sizeof sh + (size_t)h->ngames * sizeof(int32_t), (size_t)h->ngames);
+    h->bots_ready = sh.bots_ready != 0;
+    e = hipMemcpyAsync(h->ws, (const unsigned char *)src + hdr.size(), h->total, hipMemcpyDeviceToDevice, s);
+    if (e) return hip_fail(h, e, "load_state copy");
+    h->base.parked = sh.parked_any ? (uint8_t *)(h->ws + h->off_parked) : nullptr;
+    EngineParams p = h->base;
+    p.obs = obs;
+    p.mask = h->next_mask;
+    p.src_out = h->next_src;
+    e = mrts_engine_outputs(&p, s);
+    return e ? hip_fail(h, e, "load_state outputs launch") : MRTS_OK;
+}
+
 int mrts_game_stats(mrts_vec *h, void *stream, int32_t *out) {
     if (!bound(h) || !out) return fail(h, MRTS_ESTATE, "game_stats: not bound or out null");
     std::vector<int32_t> genv((size_t)h->ngames * MRTS_GENV_WORDS);

@@ -83,6 +83,7 @@ struct StepGroup {
 extern "C" {
 hipError_t mrts_engine_reset(const EngineParams *p, hipStream_t s, const int32_t *games, const int32_t *maps, int count);
 hipError_t mrts_engine_masks(const EngineParams *p, hipStream_t s);
+hipError_t mrts_engine_outputs(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step(const EngineParams *p, hipStream_t s);
 hipError_t mrts_engine_step_group(const EngineParams *ps, int n, hipStream_t s, int bots_first);
 size_t mrts_engine_group_lds_bytes(int HW, int W, int fused, int NT, int partial);

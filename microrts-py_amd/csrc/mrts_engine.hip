@@ -612,6 +612,24 @@ __global__ __launch_bounds__(NT) void k_masks(EngineParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Outputs kernel: the obs (and, when bound, the next-tick masks) of every game's
+// stored state, unchanged -- after an env-state checkpoint is restored
+// (mrts_load_state).  Parked games read zero.
+template <int NT, int P, typename OT>
+__global__ __launch_bounds__(NT) void k_outputs(EngineParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    MRTS_STAMP_NONE();
+    Lds L = carve(smem, p.HW, p.W, NT);
+    const int g = blockIdx.x;
+    if (game_parked(p, g)) {
+        zero_outputs<NT, P, OT>(p, game_of(p, g));
+        return;
+    }
+    load_game<NT>(p, L, g);
+    emit_outputs<NT, P, OT>(p, L, game_of(p, g), true, p.mask != nullptr, L.sc[SC_RES0], L.sc[SC_RES1]);
+}
+
+// ---------------------------------------------------------------------------
 // Step kernel: JNIGridnetVecClient.gameStep for one game per workgroup.
 enum : uint32_t { CAND = 1u << 31, LEGAL = 1u << 30 };
 __device__ __forceinline__ int unchecked_pos(const Grid& gd, int c, int dir) {   // UnitAction.resourceUsage position
@@ -1463,11 +1481,15 @@ __global__ __launch_bounds__(256) void k_render(const int4* __restrict__ cells, 
 // oracle's ovec_sample_actions.  `env` is the GLOBAL env index (env0 + local
 // row), so a shard of envs [env0, env0 + n) draws exactly the actions of that
 // slice of one larger run (multi-GPU sharding).
+// (each round's two 32x32 products as 64-bit ones: one v_mad_u64_u32 each instead of
+// a v_mul_hi_u32 + v_mul_lo_u32 pair, both quarter rate -- the sampler is VALU-bound
+// on its 80 multiplies per row)
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
         c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
         k0 += 0x9E3779B9u;
@@ -1750,6 +1772,14 @@ static hipError_t launch_all(const EngineParams& p, int kind, hipStream_t s, con
         }
     } else if (kind == 1) {
         hipLaunchKernelGGL((k_masks<NT>), dim3(grid), dim3(NT), sh, s, p);
+    } else if (kind == 3) {
+        if (p.partial_obs) {
+            if (p.obs_float) hipLaunchKernelGGL((k_outputs<NT, 31, float>), dim3(grid), dim3(NT), sh, s, p);
+            else hipLaunchKernelGGL((k_outputs<NT, 31, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+        } else {
+            if (p.obs_float) hipLaunchKernelGGL((k_outputs<NT, 29, float>), dim3(grid), dim3(NT), sh, s, p);
+            else hipLaunchKernelGGL((k_outputs<NT, 29, int32_t>), dim3(grid), dim3(NT), sh, s, p);
+        }
     } else {
         const bool fb = p.fuse_bots && NT > 64;
         if (fb) sh = fb_lds_bytes(p.HW, p.W, NT, !p.partial_obs && p.early_bot);
@@ -1843,6 +1873,7 @@ hipError_t mrts_engine_reset(const EngineParams* p, hipStream_t s, const int32_t
     return mrts::dispatch(*p, 0, s, games, maps, count);
 }
 hipError_t mrts_engine_masks(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 1, s, nullptr, nullptr, 0); }
+hipError_t mrts_engine_outputs(const EngineParams* p, hipStream_t s) { return mrts::dispatch(*p, 3, s, nullptr, nullptr, 0); }
 hipError_t mrts_engine_raw_obs(const EngineParams* p, hipStream_t s, int32_t* raw) {
     const int NT = p->HW <= 64 ? 64 : p->HW <= 128 ? 128 : 256;
     const size_t sh = mrts_engine_lds_bytes(p->HW, p->W);

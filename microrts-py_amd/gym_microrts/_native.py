@@ -99,6 +99,9 @@ SIGNATURES = {
     "mrts_set_bot_fusion": (ctypes.c_int, [P, ctypes.c_int32]),
     "mrts_render": (ctypes.c_int, [P, P, ctypes.c_int32, P, ctypes.c_int32]),
     "mrts_error_flags": (ctypes.c_int, [P, P, P]),
+    "mrts_state_bytes": (ctypes.c_size_t, [P]),
+    "mrts_save_state": (ctypes.c_int, [P, P, P]),
+    "mrts_load_state": (ctypes.c_int, [P, P, P, P]),
     "mrts_fused_layout_ok": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     "mrts_utt_json": (ctypes.c_char_p, [P]),
     "mrts_last_error": (ctypes.c_char_p, [P]),

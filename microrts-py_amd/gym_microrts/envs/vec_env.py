@@ -561,6 +561,39 @@ class MicroRTSGridModeVecEnv:
         nsp2 = self.num_selfplay_envs // 2
         return [2 * g, 2 * g + 1] if g < nsp2 else [self.num_selfplay_envs + g - nsp2]
 
+    def get_state(self):
+        """Env-state checkpoint (mrts_save_state; no reference counterpart):
+        a device uint8 tensor holding every game's state, the bots' pending decisions and
+        the host-side mirrors.  set_state(s) on this env brings it back."""
+        n = int(_native.lib().mrts_state_bytes(self._h))
+        if n <= 0:
+            raise _native.MicroRTSError("get_state: engine not bound")
+        buf = torch.empty(n + 256, dtype=torch.uint8, device=self.device)
+        off = (-buf.data_ptr()) % 256   # 256-byte aligned view
+        state = buf[off:off + n]
+        _native.check(_native.lib().mrts_save_state(self._h, self._stream(), state.data_ptr()), self._h, "save_state")
+        import copy
+
+        return EnvState(state, list(self._game_map), copy.deepcopy(getattr(self, "next_map", None)))
+
+    def set_state(self, state):
+        """Restore a get_state() snapshot of this env (mrts_load_state) and return the
+        restored state's obs, as reset() does; the next get_action_mask() / step()
+        continue from it bit for bit as the saved run did (map cycling included)."""
+        t = state.tensor if isinstance(state, EnvState) else None
+        if t is None or t.device != self.device or t.dtype != torch.uint8 or t.data_ptr() % 256:
+            raise ValueError("set_state expects an EnvState returned by get_state() of this env")
+        self._mask_prefetch = None
+        _native.check(_native.lib().mrts_load_state(self._h, self._stream(), t.data_ptr(), self._obs.data_ptr()), self._h,
+                      "load_state")
+        self._game_map = list(state.game_map)
+        if state.next_map is not None:
+            import copy
+
+            self.next_map = copy.deepcopy(state.next_map)
+        self._mask_fresh = self.eager_masks
+        return self._obs_out()
+
     def game_stats(self):
         """(num_games, 6) int32: game time, episode env steps, steps since creation, serial
         ticks, ordered-path rows, auto-resets (mrts_game_stats)."""
@@ -628,6 +661,15 @@ class MicroRTSGridModeVecEnv:
             self.close()
         except Exception:
             pass
+
+
+class EnvState:
+    """An env-state checkpoint (MicroRTSGridModeVecEnv.get_state): the engine's
+    snapshot (a 256-byte aligned device uint8 tensor, mrts_save_state) and the
+    Python-side map-cycling position."""
+
+    def __init__(self, tensor, game_map, next_map):
+        self.tensor, self.game_map, self.next_map = tensor, game_map, next_map
 
 
 class MicroRTSBotVecEnv(MicroRTSGridModeVecEnv):

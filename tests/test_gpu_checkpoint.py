@@ -1,0 +1,79 @@
+"""Env-state checkpoint (SURVEY.md §5 "env-state checkpoint"; no reference
+counterpart): get_state() after a stretch of play, more steps, set_state(), and the
+same actions again must repeat the first continuation bit for bit -- obs, masks,
+sources, raw rewards and dones every step -- with device bots deciding (fused and
+not), partial observability, time-limit resets inside the replayed stretch, and map
+cycling.  A snapshot of another configuration is refused."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+
+
+def _env(partial_obs=False, bot_fusion=True, cycle=False, n=32):
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+
+    bots = [microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.randomBiasedAI, microrts_ai.lightRushAI] * (n // 8)
+    kw = dict(cycle_maps=["maps/16x16/basesWorkers16x16.xml", "maps/16x16/basesWorkers16x16A.xml"]) if cycle else {}
+    return MicroRTSGridModeVecEnv(num_selfplay_envs=n // 2, num_bot_envs=len(bots), max_steps=60, ai2s=bots,
+                                  map_paths=["maps/16x16/basesWorkers16x16.xml"], partial_obs=partial_obs, reward_weight=W,
+                                  return_tensors=True, obs_dtype=torch.int32, bot_fusion=bot_fusion, **kw)
+
+
+def _run(env, s0, steps, act):
+    import torch
+
+    from gym_microrts import _native
+
+    lib, out = _native.lib(), []
+    hw = env.height * env.width
+    for s in range(s0, s0 + steps):
+        m = env.get_action_mask()
+        _native.check(lib.mrts_sample_actions_src(torch.cuda.current_stream().cuda_stream, m.data_ptr(), env._src.data_ptr(),
+                                                  env.num_envs, hw, 0, ctypes.c_uint64(5), s, act.data_ptr()))
+        o, r, d, i = env.step(act)
+        out.append((m.clone(), env._src.clone(), o.clone(), i._raw.clone(), d.clone()))
+    return out
+
+
+@pytest.mark.parametrize("partial_obs,bot_fusion,cycle", [(False, True, False), (False, False, False), (True, True, False),
+                                                           (False, True, True)])
+def test_checkpoint_replays_bit_for_bit(partial_obs, bot_fusion, cycle):
+    import torch
+
+    env = _env(partial_obs, bot_fusion, cycle)
+    env.reset()
+    act = torch.empty((env.num_envs, env.height * env.width, 7), dtype=torch.int64, device=env.device)
+    first = _run(env, 0, 45, act)
+    obs_at = first[-1][2].clone()
+    state = env.get_state()
+    a = _run(env, 45, 80, act)   # crosses the 60-step time limit: every game auto-resets inside
+    obs_back = env.set_state(state)
+    assert torch.equal(obs_back, obs_at)
+    b = _run(env, 45, 80, act)
+    for s, (x, y) in enumerate(zip(a, b)):
+        for k in range(5):
+            assert torch.equal(x[k], y[k]), f"step {45 + s} output {k}"
+    assert sum(int(x[4].sum()) for x in a) > 0
+    assert env.error_flags() == 0
+    env.close()
+
+
+def test_checkpoint_of_another_config_refused():
+    env, other = _env(n=32), _env(n=16)
+    env.reset()
+    other.reset()
+    from gym_microrts import _native
+
+    with pytest.raises(_native.MicroRTSError, match="another configuration"):
+        other.set_state(env.get_state())
+    with pytest.raises(ValueError):
+        env.set_state(object())
+    env.close()
+    other.close()
