@@ -65,7 +65,8 @@ enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_U
        SC_HAS = 31 /* units of player 0 (bits 0..15) and player 1 (16..31) */,
        SC_PSUM = 32 /* [2] cost of the player's produce rows this tick */,
        SC_PMAX = 34 /* [2] largest cost among the player's pending produces */,
-       SC_SERIAL = 36 /* the ready set executes in order */, SC_WORDS = 40 };
+       SC_SERIAL = 36 /* the ready set executes in order */, SC_NPEND = 37 /* pending produces listed in L.prod */,
+       SC_NREADY = 38 /* ready assignments listed in L.list */, SC_WORDS = 40 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -1083,6 +1084,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                     const int cost = ut_cost(code_utype(code));
                     if (cost > res_of(L, u_owner(u))) L.sc[SC_OVER] = 1;
                     if (ow == 0 || ow == 1) atomicMax(&L.sc[SC_PMAX + ow], cost);
+                    L.prod[atomicAdd(&L.sc[SC_NPEND], 1)] = c;   // (any order: issue() picks candidates by sequence)
                 }
             }
         }
@@ -1126,10 +1128,10 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
         // wider maps: the rows to decode are gathered per wave first (ballots; the
         // source words came with the prefetch, in aux) and then loaded one per lane,
         // so the lane's two to four cells cost one action-row round trip, not one each.
-        // The wave's list lives in L.list / L.prod (2 HW words, used later only by the
-        // compactions): wave w takes [w K 64, (w + 1) K 64), K = cells per lane <= 4.
+        // The wave's list lives in the ready-set snapshots' array (4 HW words, first used
+        // by the cycle): wave w takes [w K 64, (w + 1) K 64), K = cells per lane <= 4.
         const int K = (HW + NT - 1) / NT, lane = threadIdx.x & 63;
-        int32_t* const wl = L.list + (threadIdx.x >> 6) * K * 64;
+        int32_t* const wl = reinterpret_cast<int32_t*>(L.snap) + (threadIdx.x >> 6) * K * 64;
         int wn = 0;
         for (int k = 0; k < K; k++) {   // uniform trip count: every lane takes part in each ballot
             const int c = (int)threadIdx.x + k * NT;
@@ -1172,14 +1174,12 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
             if (code_type(code) == A_PRODUCE) atomicAdd(&L.sc[SC_PSUM + q], ut_cost(code_utype(code)));
         }
     }
-    // (the compaction's barrier orders the reservations, claims, SC_OVER and the
-    // bot rows before everything below; L.prod is first read by issue_player, behind
-    // the next compaction's barriers, so this one needs no trailing barrier and takes
-    // its ballot words from L.vis, free until phase A and sized for them: vis_bytes)
-    int nprod = compact_cells<NT, false>(HW, [&](int c) {
-        uint32_t a = L.act[c];
-        return a != 0 && code_type(act_code(a)) == A_PRODUCE;
-    }, L.prod, reinterpret_cast<unsigned long long*>(L.vis));
+    // the pending produces (L.prod) were appended in the decode: issue() visits its
+    // candidates by sequence word, so their order is free and no ordered compaction is
+    // needed; this barrier orders the reservations, claims, SC_OVER / SC_PSUM / SC_PMAX,
+    // L.prod and the bot rows before everything below
+    __syncthreads();
+    const int nprod = L.sc[SC_NPEND];
     // (2a) rows that interact with nothing else this tick issue lane-parallel: a
     //      row (agent or device bot) whose target position, if a move or produce,
     //      no other row (either player) and no pending assignment claims, while no
@@ -1264,11 +1264,18 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
         uint32_t a = L.act[c];
         if (a && act_done(a) <= now && code_type(act_code(a)) == A_NONE) L.act[c] = 0;
     }
-    // (the ready cells' sequence words go to L.aux, dead since the issue, in list order)
-    int nready = compact_cells<NT>(HW, [&](int c) {
-        uint32_t a = L.act[c];
-        return a != 0 && act_done(a) <= now;
-    }, L.list, L.ballot, [&](int pos, int c) { L.aux[pos] = L.seq[c]; });
+    // the ready cells in L.list, their sequence words in L.aux (dead since the issue),
+    // appended in any order: they are ranked by sequence word below
+    for (int c = threadIdx.x; c < HW; c += NT) {
+        const uint32_t a = L.act[c];
+        if (a != 0 && act_done(a) <= now) {
+            const int pos = atomicAdd(&L.sc[SC_NREADY], 1);
+            L.list[pos] = c;
+            L.aux[pos] = L.seq[c];
+        }
+    }
+    __syncthreads();
+    const int nready = L.sc[SC_NREADY];
     // snapshots of the ready assignments in LinkedHashMap (issue-sequence)
     // order: lane-parallel rank by sequence word (unique among non-NONE actions);
     // in the same pass, unitActions.remove and whether the set commutes:
