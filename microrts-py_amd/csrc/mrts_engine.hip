@@ -242,22 +242,30 @@ __device__ __forceinline__ int compact_cells(int HW, F pred, int32_t* list, unsi
 // in LDS, before the waves split): the parts of bots::bot_game's setup that are
 // per cell -- the pending assignments' reservations and produce costs
 // (isUnitActionAllowed's ResourceUsage), the free-cell words of path finding, and
-// the unit list in pgs.units order (ordered compaction by cell, then ranks by uid)
+// the unit list in pgs.units order (appended in any order, then ranked by uid)
 // -- into the bot's LDS arrays (its tail zeroed at the kernel's start); the bot
 // wave then starts at the abstract actions (bot_game, preset).  Full observability
 // only (the early path's condition), so the bot's view is the state itself.
-// `scratch`: the step's ballot words (compact_cells).
 template <int NT>
 __device__ __forceinline__ void bot_setup_workgroup(const EngineParams& p, unsigned char* smem, unsigned char* tail,
-                                                    const uint8_t* wall, unsigned long long* scratch) {
+                                                    const uint8_t* wall) {
     const int HW = p.HW, W = p.W, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const bots::BL B = bots::bot_carve(smem, HW, W, tail, false);
+    // unit list by cell (B.pa), its uids alongside (the first words of B.aa, rewritten
+    // by the bot later); B.sc[3] (zeroed with the tail) counts them
+    int32_t* const ucells = B.pa;
+    int32_t* const uids = reinterpret_cast<int32_t*>(B.aa);
     for (int base = 0; base < HW; base += NT) {
         const int c = base + (int)threadIdx.x;
         bool fr = false;
         if (c < HW) {
             const uint32_t u = B.unit[c], a = B.act[c];
             fr = !wall[c] && u == 0;
+            if (u != 0) {
+                const int pos = atomicAdd(&B.sc[3], 1);
+                ucells[pos] = c;
+                uids[pos] = B.uid[c];
+            }
             if (a) {
                 const int code = act_code(a), t = code_type(code);
                 if (t == A_MOVE || t == A_PRODUCE) {
@@ -273,11 +281,8 @@ __device__ __forceinline__ void bot_setup_workgroup(const EngineParams& p, unsig
             B.fw[(base + 64 * wv) / 32 + 1] = (uint32_t)(m >> 32);
         }
     }
-    // unit list by cell (B.pa), its uids alongside (the first words of B.aa, rewritten by the bot later)
-    int32_t* const ucells = B.pa;
-    int32_t* const uids = reinterpret_cast<int32_t*>(B.aa);
-    const int n = compact_cells<NT>(HW, [&](int c) { return B.unit[c] != 0; }, ucells, scratch,
-                                    [&](int pos, int c) { uids[pos] = B.uid[c]; });
+    __syncthreads();
+    const int n = B.sc[3];
     for (int i = threadIdx.x; i < n; i += NT) {   // rank by uid (uids are unique)
         const int u = uids[i];
         int r = 0, j = 0;
@@ -289,7 +294,6 @@ __device__ __forceinline__ void bot_setup_workgroup(const EngineParams& p, unsig
         B.ucell[r] = ucells[i];
         B.uuid[r] = u;
     }
-    if (threadIdx.x == 0) B.sc[3] = n;
 }
 
 struct Game {
@@ -1396,7 +1400,7 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     unsigned char* const tail = smem + fb_tail_offset(HW, p.W, NT, early_layout);
     if (early) {
         __syncthreads();
-        bot_setup_workgroup<NT>(p, smem, tail, L.wall, L.ballot);
+        bot_setup_workgroup<NT>(p, smem, tail, L.wall);
         __syncthreads();
         MRTS_STAMP(14, threadIdx.x == 0);
     }
