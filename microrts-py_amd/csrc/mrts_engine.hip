@@ -66,7 +66,8 @@ enum { SC_TIME = MRTS_G_TIME, SC_RES0 = MRTS_G_RES0, SC_RES1 = MRTS_G_RES1, SC_U
        SC_PSUM = 32 /* [2] cost of the player's produce rows this tick */,
        SC_PMAX = 34 /* [2] largest cost among the player's pending produces */,
        SC_SERIAL = 36 /* the ready set executes in order */, SC_NPEND = 37 /* pending produces listed in L.prod */,
-       SC_NREADY = 38 /* ready assignments listed in L.list */, SC_WORDS = 40 };
+       SC_NREADY = 38 /* ready assignments listed in L.list */, SC_NLEFT = 39 /* rows (2a) left to the ordered path */,
+       SC_WORDS = 40 };
 static_assert(MRTS_GENV_WORDS <= SC_R0, "genv words overlap the LDS scalars");
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -1200,8 +1201,10 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
     //      or its position in the bot's PlayerAction.  (A parallel produce is never
     //      a candidate of an ordered row, so it stays out of L.prod.)  Everything
     //      else takes the ordered path (2b).
+    const bool over = L.sc[SC_OVER] != 0;
     {
-        if (!L.sc[SC_OVER]) {
+        if (!over) {
+            int left = 0;   // this lane's rows left to (2b)
             for (int c = threadIdx.x; c < HW; c += NT) {
                 const uint32_t nw = L.aux[c];
                 if (!(nw & CAND)) continue;
@@ -1210,13 +1213,12 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                 const bool botrow = !G.selfplay && (q != 0 || bot0);
                 const int rank = botrow ? (int)((nw >> 12) & 0xFFFu) : c;
                 const int code = (int)(nw & 0xFFFu), ty = code_type(code);
-                if (ty == A_PRODUCE && L.sc[SC_PSUM + q] + L.sc[SC_PMAX + q] > res_of(L, q)) continue;
+                if (ty == A_PRODUCE && L.sc[SC_PSUM + q] + L.sc[SC_PMAX + q] > res_of(L, q)) { left++; continue; }
                 int n = -1;
                 if (ty == A_MOVE || ty == A_PRODUCE) {
                     const int b = unchecked_pos(gd, c, code_param(code)) + p.W;
-                    if ((L.claim[posw + (b >> 5)] >> (b & 31)) & 1u) continue;
                     n = nb_cell(gd, c, code_param(code));
-                    if (n >= 0 && L.resv[n] >= 0) continue;
+                    if (((L.claim[posw + (b >> 5)] >> (b & 31)) & 1u) || (n >= 0 && L.resv[n] >= 0)) { left++; continue; }
                 }
                 int cur = code, dur = 0;
                 if (ty == A_NONE) dur = code_param(code);
@@ -1233,12 +1235,15 @@ __device__ __forceinline__ void step_game(const EngineParams& p, const int g) {
                 }
                 L.aux[c] = nw & ~CAND;   // issued
             }
-            // no barrier: the compaction below reads each cell's aux word on the
-            // lane that wrote it, and its barriers order the rest before step (2b)
+            if (left) atomicAdd(&L.sc[SC_NLEFT], left);
         }
     }
-    // (2b) the ordered path for the rest
-    int nrows = compact_cells<NT>(HW, [&](int c) { return (L.aux[c] & CAND) != 0; }, L.list, L.ballot);
+    // (2b) the ordered path for the rest: listed (an ordered compaction, the ranks of
+    // agent rows being their cells) only when (2a) left any row -- most ticks it
+    // leaves none.  The barrier orders (2a)'s issues before the ordered part.
+    __syncthreads();
+    int nrows = 0;
+    if (over || L.sc[SC_NLEFT]) nrows = compact_cells<NT>(HW, [&](int c) { return (L.aux[c] & CAND) != 0; }, L.list, L.ballot);
     MRTS_STAMP(4, threadIdx.x == 0);
     // (2) ordered part: p0 then p1 (bot envs: the passive bot issues only NONEs)
     if (threadIdx.x == 0) {
