@@ -1498,8 +1498,9 @@ __global__ __launch_bounds__(256) void k_render(const int4* __restrict__ cells, 
 // row), so a shard of envs [env0, env0 + n) draws exactly the actions of that
 // slice of one larger run (multi-GPU sharding).
 // (each round's two 32x32 products as 64-bit ones: one v_mad_u64_u32 each instead of
-// a v_mul_hi_u32 + v_mul_lo_u32 pair, both quarter rate -- the sampler is VALU-bound
-// on its 80 multiplies per row)
+// a v_mul_hi_u32 + v_mul_lo_u32 pair, both quarter rate; the sampler's bound is its
+// memory round trips, not these multiplies: one block per row measured 32.5 -> 32.0 us,
+// profiles/r04_ab/r04u)
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
