@@ -1666,8 +1666,11 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restric
 // on basesWorkers -- while every row's 7 components are still drawn and
 // written.  One wave per 64 consecutive rows: the wave reads the rows of its
 // active lanes cooperatively (channel k on lane k, two coalesced loads per row,
-// up to four rows in flight) and folds each with two ballots.
+// up to MRTS_SRC_ROWS (4) rows in flight) and folds each with two ballots.
 constexpr int SR_WAVES = 4;
+#ifndef MRTS_SRC_ROWS
+#define MRTS_SRC_ROWS 4
+#endif
 __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n,
                                                            int hw, int env0, uint64_t seed, uint32_t step,
                                                            int64_t* __restrict__ act) {
@@ -1691,22 +1694,31 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
     const int s = in ? s_raw : 0;
     uint64_t pending = __ballot(s != 0);
     uint64_t lo = 0, hi = 0;   // this lane's row as 78 bits
-    while (pending) {          // wave-uniform
-        int r[4];
+    while (pending) {          // wave-uniform; MRTS_SRC_ROWS source rows per round trip
+        int r[MRTS_SRC_ROWS];
+        [[maybe_unused]] int cnt = 0;   // rows this trip (MRTS_SRC_NODUP)
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            r[k] = pending ? __builtin_ctzll(pending) : r[0];   // repeats r[0]: a harmless duplicate load
+        for (int k = 0; k < MRTS_SRC_ROWS; k++) {
+            cnt += pending != 0;
+            r[k] = pending ? __builtin_ctzll(pending) : r[0];   // repeats r[0]
             pending &= pending - 1ull;
         }
-        int v0[4], v1[4];
+        int v0[MRTS_SRC_ROWS], v1[MRTS_SRC_ROWS];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {   // unconditional: all eight loads in flight before the first ballot
-            const int32_t* m = mask + (row0 + r[k]) * MRTS_MASK_CH;
-            v0[k] = __builtin_nontemporal_load(m + lane);
-            v1[k] = __builtin_nontemporal_load(m + 64 + min(lane, MRTS_MASK_CH - 65));
+        for (int k = 0; k < MRTS_SRC_ROWS; k++) {   // all the loads in flight before the first ballot
+#ifdef MRTS_SRC_NODUP
+            v0[k] = v1[k] = 0;
+            if (k < cnt) {   // (wave-uniform) no duplicate loads
+#else
+            {
+#endif
+                const int32_t* m = mask + (row0 + r[k]) * MRTS_MASK_CH;
+                v0[k] = __builtin_nontemporal_load(m + lane);
+                v1[k] = __builtin_nontemporal_load(m + 64 + min(lane, MRTS_MASK_CH - 65));
+            }
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < MRTS_SRC_ROWS; k++) {
             const uint64_t b0 = __ballot(v0[k] != 0);
             const uint64_t b1 = __ballot(lane < MRTS_MASK_CH - 64 && v1[k] != 0);
             if (lane == r[k]) { lo = b0; hi = b1; }
