@@ -70,9 +70,15 @@ def parse(argv=None):
                     help="untimed ticks played before --warmup with staggered game resets, so the timed window sees "
                          "games at every phase of an episode (mid-game states, gameovers, auto-resets); "
                          "-1 = max_steps, 0 = off (every game starts fresh at the first warmup step)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process group of the timing barrier / max-over-ranks (nccl = RCCL; gloo lets several ranks "
-                         "share one GPU, as tests/test_gpu_shard.py does)")
+    ap.add_argument("--dist-backend", default="gloo", choices=["nccl", "gloo"],
+                    help="process group of the timing barrier / max-over-ranks / per-rank gather.  gloo (default): on "
+                         "the host -- the env shards exchange no data, so nothing on the data path needs RCCL and an RCCL "
+                         "init or topology problem cannot cost the scaling curve; nccl = RCCL over xGMI (each rank "
+                         "synchronises its own device first either way)")
+    ap.add_argument("--rank-timeout", type=float, default=900.0,
+                    help="seconds: a self-launched parent terminates every rank and exits 124 when they have not all "
+                         "exited by then (or STRAGGLE_S after rank 0 exited); each rank also exits 124 by itself "
+                         "after this long, so a hang under an external launcher ends too (0 = no deadline)")
     ap.add_argument("--bucket-streams", type=int, default=0, choices=[0, 1],
                     help="mixed workload: 1 = each size bucket on its own HIP stream (concurrent), 0 = back to back")
     ap.add_argument("--group-policy", default="default",
@@ -532,13 +538,38 @@ def _free_port():
         return so.getsockname()[1]
 
 
-def launch_ranks(n, argv, popen=None, poll_s=0.2):
+# a self-launched parent waits at most this long for the other ranks once rank 0 has exited
+STRAGGLE_S = 60.0
+
+
+def _stop(procs, rcs, grace_s=30):
+    """terminate every rank still running, then kill what ignores it"""
+    import subprocess
+
+    for r, p in enumerate(procs):
+        if rcs[r] is None:
+            p.terminate()
+    for r, p in enumerate(procs):
+        if rcs[r] is None:
+            try:
+                rcs[r] = p.wait(timeout=grace_s)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                rcs[r] = p.wait()
+
+
+def launch_ranks(n, argv, popen=None, poll_s=0.2, deadline_s=900.0, clock=time.monotonic):
     """`bench.py --gpus N` without a launcher: start ranks 0..N-1 of this same
     command as fresh child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
     in their environment, as torch.distributed.run sets them), relay their output,
     and return the worst exit status.  Runs before the parent imports torch, so the
     parent never initialises HIP (children start from a clean process; no exec).
-    When a rank fails, the others are terminated (they would wait in the barrier)."""
+    Every rank is terminated, the per-rank statuses printed and a non-zero status
+    returned when
+      * a rank fails (the others would wait in the barrier): that rank's status;
+      * `deadline_s` passes with a rank still running (0 = no deadline): 124;
+      * rank 0 (which prints the line) exited and another rank is still running
+        STRAGGLE_S later: 124."""
     import subprocess
 
     popen = popen or subprocess.Popen
@@ -549,31 +580,65 @@ def launch_ranks(n, argv, popen=None, poll_s=0.2):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port, MICRORTS_BENCH_SELF_LAUNCHED="1")
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    t0 = clock()
     rcs = [None] * n
-    cause = 0   # the status of the first rank seen failing (the others are then stopped)
+    cause, why = 0, ""
+    rank0_done = None
     while any(rc is None for rc in rcs):
         for r, p in enumerate(procs):
             if rcs[r] is None:
                 rcs[r] = p.poll()
                 if rcs[r] not in (None, 0) and not cause:
-                    cause = rcs[r]
+                    cause, why = rcs[r], f"rank {r} failed"
+        now = clock()
+        if rcs[0] is not None and rank0_done is None:
+            rank0_done = now
+        if not cause and any(rc is None for rc in rcs):
+            if deadline_s and now - t0 > deadline_s:
+                cause, why = 124, f"deadline of {deadline_s:g} s passed"
+            elif rank0_done is not None and now - rank0_done > STRAGGLE_S:
+                cause, why = 124, f"rank 0 exited {STRAGGLE_S:g} s ago"
         if cause:
-            for r, p in enumerate(procs):
-                if rcs[r] is None:
-                    p.terminate()
-            for r, p in enumerate(procs):
-                if rcs[r] is None:
-                    try:
-                        rcs[r] = p.wait(timeout=30)
-                    except subprocess.TimeoutExpired:
-                        p.kill()
-                        rcs[r] = p.wait()
-            break
+            hung = [r for r, rc in enumerate(rcs) if rc is None]
+            _stop(procs, rcs)
+            print(f"bench.py: {why}; ranks still running then: {hung}; rank exit statuses {rcs}", file=sys.stderr,
+                  flush=True)
+            return cause if cause > 0 else 128 - cause   # killed by signal k: 128 + k, as a shell reports it
         time.sleep(poll_s)
-    if cause:
-        print(f"bench.py: rank exit statuses {rcs}", file=sys.stderr)
-        return cause if cause > 0 else 128 - cause   # killed by signal k: 128 + k, as a shell reports it
     return 0
+
+
+def _rank_watchdog(seconds, rank):
+    """A rank's own deadline (--rank-timeout): under an external launcher nothing else
+    ends a rank stuck in a rendezvous, a collective or a kernel.  Exits the process
+    with 124 (no exec; the GPU context is torn down as at any exit)."""
+    import threading
+
+    def fire():
+        print(f"bench.py: rank {rank} still running after --rank-timeout {seconds:g} s; exiting 124", file=sys.stderr,
+              flush=True)
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def gather_per_rank(elapsed, n_envs, steps, world, dev):
+    """Every rank's elapsed time and env-steps/s (one all_gather), so a straggler can be
+    told from a uniform slowdown in the one line rank 0 prints."""
+    if world == 1:
+        vals = [elapsed]
+    else:
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=_coll_device(dev))
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        vals = [float(x.item()) for x in out]
+    return [{"rank": r, "elapsed_s": round(v, 6), "env_steps_per_s": round(n_envs * steps / v, 1)} for r, v in enumerate(vals)]
 
 
 def main(argv=None):
@@ -584,7 +649,7 @@ def main(argv=None):
     args = parse(argv)
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
-            return launch_ranks(args.gpus, argv)
+            return launch_ranks(args.gpus, argv, deadline_s=args.rank_timeout)
         world = 1
     else:
         world = int(os.environ["WORLD_SIZE"])
@@ -593,6 +658,8 @@ def main(argv=None):
             return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.rank_timeout > 0:
+        _rank_watchdog(args.rank_timeout, rank)
     import torch
 
     # one GPU per rank; ranks beyond the visible GPUs share them (gloo shard tests on a 1-GPU box)
@@ -602,11 +669,15 @@ def main(argv=None):
     if world > 1:
         import torch.distributed as dist
 
+        import datetime
+
         torch.cuda.set_device(local_rank)
+        # rendezvous / collective timeout well inside the rank's own deadline
+        tmo = datetime.timedelta(seconds=max(60.0, min(600.0, args.rank_timeout or 600.0)))
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=tmo)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         pg = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "visible_devices": ndev,
               "launcher": "bench.py (self-launched ranks)" if os.environ.get("MICRORTS_BENCH_SELF_LAUNCHED")
               else "external (torch.distributed.run or equivalent)"}
@@ -630,6 +701,7 @@ def main(argv=None):
                 flags |= r[2]
     dev = torch.device("cuda", local_rank)
     elapsed_max = max_over_ranks(elapsed, world, dev)
+    per_rank = gather_per_rank(elapsed, N, args.steps, world, dev)
     total_env_steps = world * N * args.steps
     value = total_env_steps / elapsed_max
     out = None
@@ -713,6 +785,10 @@ def main(argv=None):
             "engine_error_flags": flags,
             "window": stats,
         }
+        stats["per_rank"] = per_rank
+        if world > 1:
+            el = [p["elapsed_s"] for p in per_rank]
+            stats["per_rank_spread"] = round(max(el) / min(el), 4)   # slowest / fastest rank
         if args.workload != "selfplay":
             out["metric"] = f"env-steps/sec, workload {args.workload} (secondary config, not the BASELINE metric)"
         if args.api != "tensor":

@@ -70,6 +70,28 @@ class GridNet(nn.Module):
         self.v = nn.Sequential(nn.Flatten(), orthogonal(nn.Linear(64 * (h // 4) * (w // 4), 128)), nn.ReLU(),
                                orthogonal(nn.Linear(128, 1), 1.0))
 
+    # ppo_gridnet.py's Agent (experiments/ppo_gridnet.py:191-212) names the same layers
+    # encoder.{1,4} (after its Transpose), actor.{0,2}, critic.{1,3}
+    REFERENCE_NAMES = {"encoder.1": "enc.0", "encoder.4": "enc.3", "actor.0": "pi.0", "actor.2": "pi.2",
+                       "critic.1": "v.1", "critic.3": "v.3"}
+
+    def load_reference_state(self, tensors):
+        """Load a reference Agent state_dict (name -> tensor / array, e.g. the
+        tests/golden/agent_sota_policy.npz fixture of agent_sota.pt); layers it does
+        not hold keep their values.  Returns the names loaded."""
+        own = self.state_dict()
+        done = []
+        for k, v in tensors.items():
+            layer, _, field = k.rpartition(".")
+            if layer in self.REFERENCE_NAMES:
+                name = f"{self.REFERENCE_NAMES[layer]}.{field}"
+                t = torch.as_tensor(np.asarray(v))
+                assert own[name].shape == t.shape, (k, tuple(t.shape), tuple(own[name].shape))
+                own[name] = t
+                done.append(k)
+        self.load_state_dict(own)
+        return done
+
     def forward(self, obs):
         z = self.enc(obs.permute(0, 3, 1, 2))
         logits = self.pi(z).permute(0, 2, 3, 1).reshape(obs.shape[0] * self.hw, sum(NVEC))

@@ -244,7 +244,9 @@ int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t si
  * mirrors -- copied into / out of a caller device buffer of mrts_state_bytes(h)
  * bytes (256-byte aligned).  mrts_save_state synchronises the stream.
  * mrts_load_state restores a snapshot of the same configuration and map table
- * into this handle (MRTS_EINVAL otherwise) and writes the restored state's obs
+ * into this handle -- same env split, obs layout, game offset, bots (both players)
+ * and map templates, checked by a fingerprint in the snapshot's header; MRTS_EINVAL
+ * otherwise, before anything but the fixed header is read -- and writes the restored state's obs
  * into `obs` (and its next-tick masks into the bound mask outputs), as mrts_reset
  * does for a fresh state; stepping on from it repeats the saved run bit for bit. */
 size_t mrts_state_bytes(const mrts_vec *h);

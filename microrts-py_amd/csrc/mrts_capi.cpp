@@ -149,12 +149,9 @@ std::string utt_json() {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// int4 records between consecutive games' cell rows: HW plus MRTS_CELL_PAD (A/B
-// experiments on the HBM placement of the per-game rows)
-#ifndef MRTS_CELL_PAD
-#define MRTS_CELL_PAD 0
-#endif
-int cell_stride(int HW) { return HW + MRTS_CELL_PAD; }
+// int4 records between consecutive games' cell rows (a padded stride measured
+// neutral, profiles/r04_ab/README.md)
+int cell_stride(int HW) { return HW; }
 
 }  // namespace
 
@@ -729,17 +726,48 @@ int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t si
 }
 
 // Env-state checkpoint: [header | workspace bytes].  The header carries what the
-// host holds beside the workspace (bots_ready, the games' map indices, parked flags)
-// and the shape the snapshot belongs to.
+// host holds beside the workspace (bots_ready, the games' map indices, parked flags),
+// the shape the snapshot belongs to and a fingerprint of the configuration whose
+// device tables the workspace copy brings along (bots, map templates): a snapshot
+// loads only into a handle of the same shape AND configuration.
 namespace {
 struct StateHeader {
     uint32_t magic, version;
     int32_t ngames, HW, nmaps, bots_ready, parked_any;
     uint64_t total;
+    uint64_t config;   // config_fingerprint
 };
 const uint32_t kStateMagic = 0x4d525453u;   // "MRTS"
+const uint32_t kStateVersion = 2;
 size_t state_header_bytes(const mrts_vec *h) {
     return align256(sizeof(StateHeader) + (size_t)h->ngames * (sizeof(int32_t) + 1));
+}
+struct Fnv {
+    uint64_t v = 1469598103934665603ull;
+    void bytes(const void *p, size_t n) {
+        const unsigned char *b = (const unsigned char *)p;
+        for (size_t i = 0; i < n; i++) v = (v ^ b[i]) * 1099511628211ull;
+    }
+    void i32(int32_t x) { bytes(&x, sizeof x); }
+};
+// FNV-1a over everything a workspace copy would carry in besides the game states:
+// env split, obs layout, global game offset (bot RNG streams), the bots of every bot
+// env (both players), the map table's capacity and every map template (size,
+// resources, walls, unit records)
+uint64_t config_fingerprint(const mrts_vec *h) {
+    Fnv f;
+    for (int32_t x : {h->nsp, h->nbot, h->partial_obs, h->obs_float, h->game_offset, h->map_capacity, h->W, h->H}) f.i32(x);
+    f.i32((int32_t)h->bot_ai.size());
+    f.bytes(h->bot_ai.data(), h->bot_ai.size() * sizeof(int32_t));
+    f.i32((int32_t)h->bot_ai0.size());
+    f.bytes(h->bot_ai0.data(), h->bot_ai0.size() * sizeof(int32_t));
+    f.i32((int32_t)h->maps.size());
+    for (const MapData &m : h->maps) {
+        for (int32_t x : {m.w, m.h, m.res[0], m.res[1], m.nunits}) f.i32(x);
+        f.bytes(m.wall.data(), m.wall.size());
+        f.bytes(m.cells.data(), m.cells.size() * sizeof(int4));
+    }
+    return f.v;
 }
 }  // namespace
 
@@ -749,8 +777,8 @@ int mrts_save_state(mrts_vec *h, void *stream, void *dst) {
     if (!bound(h) || !dst) return fail(h, MRTS_ESTATE, "save_state: workspace not bound or dst null");
     if (((uintptr_t)dst & 255u) != 0) return fail(h, MRTS_EINVAL, "save_state: dst must be 256-byte aligned");
     std::vector<unsigned char> hdr(state_header_bytes(h), 0);
-    StateHeader sh{kStateMagic, 1, h->ngames, h->HW, (int32_t)h->maps.size(), h->bots_ready ? 1 : 0,
-                   h->base.parked != nullptr ? 1 : 0, (uint64_t)h->total};
+    StateHeader sh{kStateMagic, kStateVersion, h->ngames, h->HW, (int32_t)h->maps.size(), h->bots_ready ? 1 : 0,
+                   h->base.parked != nullptr ? 1 : 0, (uint64_t)h->total, config_fingerprint(h)};
     std::memcpy(hdr.data(), &sh, sizeof sh);
     std::memcpy(hdr.data() + sizeof sh, h->game_map.data(), (size_t)h->ngames * sizeof(int32_t));
     std::memcpy(hdr.data() + sizeof sh + (size_t)h->ngames * sizeof(int32_t), h->parked.data(), (size_t)h->ngames);
@@ -758,7 +786,10 @@ int mrts_save_state(mrts_vec *h, void *stream, void *dst) {
     unsigned char *d = (unsigned char *)dst;
     hipError_t e = hipMemcpyAsync(d, hdr.data(), hdr.size(), hipMemcpyHostToDevice, s);
     if (!e) e = hipMemcpyAsync(d + hdr.size(), h->ws, h->total, hipMemcpyDeviceToDevice, s);
-    if (!e) e = hipStreamSynchronize(s);   // the host header buffer is this call's
+    // the host header buffer is this call's: drain the stream on every path (a queued
+    // copy may still read it after a later enqueue failed)
+    const hipError_t es = hipStreamSynchronize(s);
+    if (!e) e = es;
     return e ? hip_fail(h, e, "save_state copy") : MRTS_OK;
 }
 
@@ -766,15 +797,23 @@ int mrts_load_state(mrts_vec *h, void *stream, const void *src, void *obs) {
     if (!bound(h) || !src || !obs) return fail(h, MRTS_ESTATE, "load_state: workspace not bound or null buffer");
     if (((uintptr_t)src & 255u) != 0) return fail(h, MRTS_EINVAL, "load_state: src must be 256-byte aligned");
     hipStream_t s = (hipStream_t)stream;
-    std::vector<unsigned char> hdr(state_header_bytes(h), 0);
-    hipError_t e = hipMemcpyAsync(hdr.data(), src, hdr.size(), hipMemcpyDeviceToHost, s);
+    // the fixed header first: a snapshot of a smaller handle is shorter than this
+    // handle's header, so nothing beyond sizeof(StateHeader) is read before it checks out
+    StateHeader sh;
+    hipError_t e = hipMemcpyAsync(&sh, src, sizeof sh, hipMemcpyDeviceToHost, s);
     if (!e) e = hipStreamSynchronize(s);
     if (e) return hip_fail(h, e, "load_state header");
-    StateHeader sh;
-    std::memcpy(&sh, hdr.data(), sizeof sh);
-    if (sh.magic != kStateMagic || sh.version != 1 || sh.ngames != h->ngames || sh.HW != h->HW || sh.nmaps != (int32_t)h->maps.size() ||
-        sh.total != (uint64_t)h->total)
+    if (sh.magic != kStateMagic || sh.version != kStateVersion)
+        return fail(h, MRTS_EINVAL, "load_state: not a snapshot of this library version (mrts_save_state)");
+    if (sh.ngames != h->ngames || sh.HW != h->HW || sh.nmaps != (int32_t)h->maps.size() || sh.total != (uint64_t)h->total)
         return fail(h, MRTS_EINVAL, "load_state: the snapshot belongs to another configuration or map table");
+    if (sh.config != config_fingerprint(h))
+        return fail(h, MRTS_EINVAL, "load_state: the snapshot belongs to another configuration (bots, maps, obs layout "
+                                    "or game offset differ)");
+    std::vector<unsigned char> hdr(state_header_bytes(h), 0);
+    e = hipMemcpyAsync(hdr.data(), src, hdr.size(), hipMemcpyDeviceToHost, s);
+    if (!e) e = hipStreamSynchronize(s);
+    if (e) return hip_fail(h, e, "load_state header");
     std::memcpy(h->game_map.data(), hdr.data() + sizeof sh, (size_t)h->ngames * sizeof(int32_t));
     std::memcpy(h->parked.data(), hdr.data() + sizeof sh + (size_t)h->ngames * sizeof(int32_t), (size_t)h->ngames);
     h->bots_ready = sh.bots_ready != 0;

@@ -32,7 +32,6 @@ import os
 import warnings
 import xml.etree.ElementTree as ET
 from enum import Enum
-from itertools import cycle
 
 import numpy as np
 import torch
@@ -223,7 +222,7 @@ class MicroRTSGridModeVecEnv:
             raise MicroRTSNotImplemented("prior_mode other than 'none' (KG prior) is out of scope")
         self.microrts_path = os.path.join(gym_microrts.__path__[0], "microrts")
         self.cycle_maps = list(map(lambda i: os.path.join(self.microrts_path, i), cycle_maps))
-        self.next_map = cycle(self.cycle_maps)
+        self.next_map = MapCycle(self.cycle_maps)
 
         # read map (vec_env.py:148-150)
         first = os.path.join(self.microrts_path, self.map_paths[0])
@@ -572,9 +571,7 @@ class MicroRTSGridModeVecEnv:
         off = (-buf.data_ptr()) % 256   # 256-byte aligned view
         state = buf[off:off + n]
         _native.check(_native.lib().mrts_save_state(self._h, self._stream(), state.data_ptr()), self._h, "save_state")
-        import copy
-
-        return EnvState(state, list(self._game_map), copy.deepcopy(getattr(self, "next_map", None)))
+        return EnvState(state, list(self._game_map), self.next_map.drawn)
 
     def set_state(self, state):
         """Restore a get_state() snapshot of this env (mrts_load_state) and return the
@@ -583,14 +580,14 @@ class MicroRTSGridModeVecEnv:
         t = state.tensor if isinstance(state, EnvState) else None
         if t is None or t.device != self.device or t.dtype != torch.uint8 or t.data_ptr() % 256:
             raise ValueError("set_state expects an EnvState returned by get_state() of this env")
+        if t.numel() != int(_native.lib().mrts_state_bytes(self._h)) or not t.is_contiguous():
+            raise ValueError("set_state: the snapshot's size differs from this env's (another configuration)")
         self._mask_prefetch = None
         _native.check(_native.lib().mrts_load_state(self._h, self._stream(), t.data_ptr(), self._obs.data_ptr()), self._h,
                       "load_state")
         self._game_map = list(state.game_map)
         if state.next_map is not None:
-            import copy
-
-            self.next_map = copy.deepcopy(state.next_map)
+            self.next_map = MapCycle(self.cycle_maps, state.next_map)
         self._mask_fresh = self.eager_masks
         return self._obs_out()
 
@@ -663,10 +660,29 @@ class MicroRTSGridModeVecEnv:
             pass
 
 
+class MapCycle:
+    """itertools.cycle(maps) (vec_env.py's `self.next_map`) that counts the maps drawn,
+    so an env-state checkpoint stores the cycling position as an integer and restores
+    it without copying an iterator (copying itertools objects is gone in Python 3.14)."""
+
+    def __init__(self, maps, drawn=0):
+        self.maps, self.drawn = list(maps), int(drawn)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if not self.maps:
+            raise StopIteration
+        m = self.maps[self.drawn % len(self.maps)]
+        self.drawn += 1
+        return m
+
+
 class EnvState:
     """An env-state checkpoint (MicroRTSGridModeVecEnv.get_state): the engine's
     snapshot (a 256-byte aligned device uint8 tensor, mrts_save_state) and the
-    Python-side map-cycling position."""
+    Python-side map-cycling position (maps drawn from `next_map` so far)."""
 
     def __init__(self, tensor, game_map, next_map):
         self.tensor, self.game_map, self.next_map = tensor, game_map, next_map
@@ -954,7 +970,7 @@ class MicroRTSSizeCyclingVecEnv:
         self.sizes = sorted({size(m) for m in per_env + list(cycle_maps)})
         self._size_of = {m: size(m) for m in per_env + list(cycle_maps)}
         self.cycle_maps = list(cycle_maps)
-        self.next_map = cycle(self.cycle_maps)
+        self.next_map = MapCycle(self.cycle_maps)
         self.bucket = np.array([self.sizes.index(self._size_of[m]) for m in per_env], np.int64)
         self.envs = []
         for i, sz in enumerate(self.sizes):

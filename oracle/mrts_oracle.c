@@ -94,6 +94,7 @@ typedef struct { /* rts.GameState + rts.PhysicalGameState */
     int *grid; /* cell -> unit slot, -1 if empty                              */
     OAssign *as;
     int na, capa;
+    int64_t ev[OEV_N]; /* event counters (ovec_event_counts); survive resets       */
 } OGS;
 
 struct OVec {
@@ -506,6 +507,7 @@ static void issue(OGS *g, OPA *pa) {
             ru_free(&ur);
             if (ok) continue;
             if (uaa->time == g->time) { /* same cycle: CANCEL_BOTH */
+                g->ev[OEV_CANCEL_BOTH]++;
                 int d1 = eta(&g->u[uaa->unit], &uaa->act);
                 int d2 = eta(&g->u[p->unit], &p->act);
                 int d = d1 < d2 ? d1 : d2;
@@ -518,6 +520,7 @@ static void issue(OGS *g, OPA *pa) {
                 p->act = act_none(d); /* p = new Pair(...): pa keeps the old action */
             } else {
                 /* "Inconsistent actions were executed!": p.m_b = new UnitAction(NONE) */
+                g->ev[OEV_INCONSISTENT]++;
                 p->act = act_none(DIRECTION_NONE);
             }
         }
@@ -563,7 +566,11 @@ static void execute(OGS *g, int ui, const OAct *a) {
         if (o >= 0) {
             /* VERSION_ORIGINAL: minDamage == maxDamage, no RNG draw */
             g->u[o].hp -= UT[u->type].min_dmg;
-            if (g->u[o].hp <= 0) remove_unit(g, o);
+            if (u->player >= 0) g->ev[OEV_HITS + u->player]++;
+            if (g->u[o].hp <= 0) {
+                if (u->player >= 0) g->ev[OEV_KILLS + u->player]++;
+                remove_unit(g, o);
+            }
         }
         break;
     }
@@ -592,6 +599,7 @@ static void execute(OGS *g, int ui, const OAct *a) {
         int tx = u->x + (a->param == D_RIGHT) - (a->param == D_LEFT);
         int ty = u->y + (a->param == D_DOWN) - (a->param == D_UP);
         int owner = u->player; /* add_unit may move the unit pool */
+        if (owner >= 0) g->ev[OEV_PRODUCED + 7 * owner + a->utype]++;
         add_unit(g, a->utype, owner, tx, ty, 0, UT[a->utype].hp);
         g->res[owner] -= UT[a->utype].cost;
         break;
@@ -825,6 +833,12 @@ void ovec_reset_game(OVec *v, int game, int map_id) {
     v->env_steps[game] = 0;
     v->aam[2 * game].n = v->aam[2 * game + 1].n = 0; /* ai1/ai2.reset() */
     game_obs(v, game);
+}
+
+void ovec_event_counts(const OVec *v, int64_t *out) {
+    for (int k = 0; k < OEV_N; k++) out[k] = 0;
+    for (int g = 0; g < v->ngames; g++)
+        for (int k = 0; k < OEV_N; k++) out[k] += v->gs[g].ev[k];
 }
 
 void ovec_reset(OVec *v) {

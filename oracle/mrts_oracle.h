@@ -92,6 +92,15 @@ void ovec_sample_actions(const int32_t *masks78, int n, int hw, int env0, uint64
 void ovec_bench_steps(OVec *v, int steps, uint64_t seed, uint32_t step0, int32_t *masks79, int64_t *act, int32_t *src,
                       double *reward, uint8_t *done, int32_t *obs);
 
+/* Trajectory statistics (test diagnostics, not part of the restated API): event
+ * counts summed over every game since creation, resets included.
+ * [OEV_CANCEL_BOTH] issue's same-cycle conflicts (both actions -> NONE),
+ * [OEV_INCONSISTENT] issue's conflicts with an older assignment (new -> NONE),
+ * [OEV_PRODUCED + 7 * player + type] units produced (executed), by type,
+ * [OEV_HITS + player] attacks that hit a unit, [OEV_KILLS + player] units killed. */
+enum { OEV_CANCEL_BOTH = 0, OEV_INCONSISTENT = 1, OEV_PRODUCED = 2, OEV_HITS = 16, OEV_KILLS = 18, OEV_N = 20 };
+void ovec_event_counts(const OVec *v, int64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

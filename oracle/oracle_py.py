@@ -51,6 +51,7 @@ def lib():
         L.ovec_dump_cells.argtypes = [P, ctypes.c_int, P]
         L.ovec_sample_actions.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P]
         L.ovec_bench_steps.argtypes = [P, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, P, P, P, P, P, P]
+        L.ovec_event_counts.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -189,6 +190,16 @@ class OracleVecEnv:
         lib().ovec_bench_steps(self._h, steps, ctypes.c_uint64(seed), ctypes.c_uint32(step0), ptr(m), ptr(a), ptr(src),
                                ptr(rew), ptr(done), ptr(obs))
         return obs, rew, done.astype(bool)
+
+    def event_counts(self):
+        """Trajectory statistics summed over every game (ovec_event_counts): CANCEL_BOTH and
+        inconsistent-issue conflicts, units produced per player and type, hits, kills."""
+        c = np.zeros(20, np.int64)
+        lib().ovec_event_counts(self._h, ptr(c))
+        prod = c[2:16].reshape(2, 7)
+        return {"cancel_both": int(c[0]), "inconsistent": int(c[1]),
+                "produced": [{t: int(prod[p, i]) for i, t in enumerate(UNIT_TYPES)} for p in range(2)],
+                "hits": [int(c[16]), int(c[17])], "kills": [int(c[18]), int(c[19])]}
 
     def dump_cells(self, g):
         out = np.zeros((self.height * self.width, 8), np.int32)

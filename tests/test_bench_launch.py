@@ -5,12 +5,13 @@ touched the GPU must not fork/exec the ranks' runtime state, and the children
 each pick their own device): these tests run bench.main with `torch` replaced
 by a module that raises on any attribute access, and with subprocess.Popen
 replaced by a recorder, so they need no GPU.  The GPU end-to-end check (the
-self-launched ranks' dumps are the halves of a 1-rank run) is
-tests/test_gpu_shard.py::test_bench_self_launch_end_to_end.
+self-launched ranks' dumps are the slices of a 1-rank run) is
+tests/test_gpu_shard.py::test_bench_sharding_end_to_end.
 """
 import os
 import subprocess
 import sys
+import time
 import types
 
 import pytest
@@ -100,3 +101,56 @@ def test_one_gpu_does_not_spawn(monkeypatch):
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     args = bench.parse(["--gpus", "1", "--roofline-steps", "64"])
     assert args.gpus == 1 and args.roofline_steps == 64 and not args.no_kernel_events
+
+
+def test_self_launch_hung_rank_hits_the_deadline(no_torch, monkeypatch, capsys):
+    """A rank that neither exits nor fails (an RCCL init hang, a stuck kernel): the
+    parent terminates every rank and exits non-zero once --rank-timeout passes."""
+    procs = []
+
+    def popen(cmd, env=None, **kw):
+        p = _FakeProc(None)   # never exits until terminated
+        procs.append(p)
+        return p
+
+    monkeypatch.setattr(subprocess, "Popen", popen)
+    t0 = time.monotonic()
+    rc = bench.main(["--gpus", "4", "--rank-timeout", "0.5"])
+    assert rc == 124 and time.monotonic() - t0 < 5
+    assert all(p.terminated for p in procs)
+    err = capsys.readouterr().err
+    assert "deadline" in err and "[0, 1, 2, 3]" in err
+
+
+def test_self_launch_straggler_after_rank0(no_torch, monkeypatch, capsys):
+    """Rank 0 (which prints the line) exited but rank 2 never does: the parent stops it
+    STRAGGLE_S later and exits 124 rather than waiting for the driver's time limit."""
+    monkeypatch.setattr(bench, "STRAGGLE_S", 0.3)
+    procs = []
+
+    def popen(cmd, env=None, **kw):
+        p = _FakeProc(None if env["RANK"] == "2" else 0)
+        procs.append(p)
+        return p
+
+    monkeypatch.setattr(subprocess, "Popen", popen)
+    t0 = time.monotonic()
+    assert bench.main(["--gpus", "4"]) == 124
+    assert time.monotonic() - t0 < 5
+    assert [p.terminated for p in procs] == [False, False, True, False]
+    assert "rank 0 exited" in capsys.readouterr().err
+
+
+def test_dist_backend_defaults_to_gloo():
+    """The timing barrier / max-over-ranks / per-rank gather run on gloo unless asked:
+    no data-path collective exists, so RCCL is not needed for the curve."""
+    a = bench.parse(["--gpus", "8"])
+    assert a.dist_backend == "gloo" and a.rank_timeout == 900.0
+    assert bench.parse(["--dist-backend", "nccl"]).dist_backend == "nccl"
+
+
+def test_per_rank_single():
+    import torch as _t  # noqa: F401  (real torch: gather_per_rank at world 1 makes no collective)
+
+    pr = bench.gather_per_rank(0.5, 8192, 100, 1, None)
+    assert pr == [{"rank": 0, "elapsed_s": 0.5, "env_steps_per_s": 8192 * 100 / 0.5}]

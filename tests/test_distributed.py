@@ -32,13 +32,14 @@ def _worker(rank, world, port, q):
     dev = torch.device("cpu")
     bench.barrier(world, dev)
     m = bench.max_over_ranks(1.5 + rank, world, dev)
+    per_rank = bench.gather_per_rank(1.0 + rank, 100, 10, world, dev)
     env0, game0 = bench.shard(rank, 8192, 8192, 0)
     # the staggered pre-roll: each rank resets its slice of the global plan
     plan = bench.stagger_plan(4096, 2000, game0, world * 4096)
     resets = [(t, game0 + g) for t, gs in enumerate(plan) for g in gs]
     bench.barrier(world, dev)
     dist.destroy_process_group()
-    q.put((rank, m, env0, game0, resets))
+    q.put((rank, m, env0, game0, resets, per_rank))
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -55,6 +56,9 @@ def test_bench_collectives_gloo(world):
         assert p.exitcode == 0
     # every rank sees the max elapsed time; shards are disjoint, contiguous, even
     assert all(r[1] == 1.5 + world - 1 for r in res)
+    # every rank gathers every rank's elapsed time / rate (bench line: window.per_rank)
+    assert all(r[5] == [{"rank": k, "elapsed_s": 1.0 + k, "env_steps_per_s": round(1000 / (1.0 + k), 1)}
+                        for k in range(world)] for r in res)
     assert [(r[2], r[3]) for r in res] == [(k * 8192, k * 4096) for k in range(world)]
     # the ranks' staggered resets together are exactly one unsharded run's plan
     import sys

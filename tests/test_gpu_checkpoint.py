@@ -13,16 +13,16 @@ pytestmark = pytest.mark.gpu
 W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
 
 
-def _env(partial_obs=False, bot_fusion=True, cycle=False, n=32):
+def _env(partial_obs=False, bot_fusion=True, cycle=False, n=32, bots=None, map_path="maps/16x16/basesWorkers16x16.xml"):
     import torch
 
     from gym_microrts import microrts_ai
     from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
 
-    bots = [microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.randomBiasedAI, microrts_ai.lightRushAI] * (n // 8)
+    bots = bots or [microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.randomBiasedAI, microrts_ai.lightRushAI] * (n // 8)
     kw = dict(cycle_maps=["maps/16x16/basesWorkers16x16.xml", "maps/16x16/basesWorkers16x16A.xml"]) if cycle else {}
     return MicroRTSGridModeVecEnv(num_selfplay_envs=n // 2, num_bot_envs=len(bots), max_steps=60, ai2s=bots,
-                                  map_paths=["maps/16x16/basesWorkers16x16.xml"], partial_obs=partial_obs, reward_weight=W,
+                                  map_paths=[map_path], partial_obs=partial_obs, reward_weight=W,
                                   return_tensors=True, obs_dtype=torch.int32, bot_fusion=bot_fusion, **kw)
 
 
@@ -66,14 +66,50 @@ def test_checkpoint_replays_bit_for_bit(partial_obs, bot_fusion, cycle):
 
 
 def test_checkpoint_of_another_config_refused():
+    import torch
+
+    from gym_microrts import _native
+
     env, other = _env(n=32), _env(n=16)
     env.reset()
     other.reset()
-    from gym_microrts import _native
-
-    with pytest.raises(_native.MicroRTSError, match="another configuration"):
-        other.set_state(env.get_state())
+    big, small = env.get_state(), other.get_state()
+    with pytest.raises(ValueError, match="another configuration"):
+        other.set_state(big)
     with pytest.raises(ValueError):
         env.set_state(object())
+    # below the Python check: the C ABI reads only the fixed header of a foreign snapshot
+    # (a smaller handle's snapshot is shorter than this handle's header) and refuses it
+    lib, st = _native.lib(), torch.cuda.current_stream().cuda_stream
+    for h, snap, obs in ((env._h, small, env._obs), (other._h, big, other._obs)):
+        assert lib.mrts_load_state(h, st, snap.tensor.data_ptr(), obs.data_ptr()) == -1   # MRTS_EINVAL
+    env.close()
+    other.close()
+
+
+@pytest.mark.parametrize("what", ["bots", "map", "partial_obs"])
+def test_checkpoint_same_shape_other_config_refused(what):
+    """a snapshot of a handle with the same shape (games, cells, map count,
+    workspace size) but other bots, another map or another obs layout would copy that
+    handle's device tables in; the header's configuration fingerprint refuses it."""
+    from gym_microrts import _native, microrts_ai
+
+    env = _env(n=32)
+    if what == "bots":
+        other = _env(n=32, bots=[microrts_ai.workerRushAI] * 16)
+    elif what == "map":
+        other = _env(n=32, map_path="maps/16x16/basesWorkers16x16A.xml")
+    else:
+        other = _env(n=32, partial_obs=True)
+    env.reset()
+    other.reset()
+    snap = env.get_state()
+    if snap.tensor.numel() == int(_native.lib().mrts_state_bytes(other._h)):
+        with pytest.raises(_native.MicroRTSError, match="another configuration"):
+            other.set_state(snap)
+    else:
+        with pytest.raises(ValueError, match="another configuration"):
+            other.set_state(snap)
+    env.set_state(snap)   # its own snapshot still loads
     env.close()
     other.close()

@@ -195,3 +195,84 @@ def test_fullsize_headline_8192_staggered_2000_ticks():
     assert g.error_flags() == 0
     g.close()
     o.close()
+
+
+@pytest.mark.timeout(1200)
+def test_fullsize_mixed_buckets_bench_split_8192():
+    """configs[4] at the bench's own size and launch plan: bench.py's
+    mixed workload exactly -- 8192 envs split 2048 / 4096 / 2048 over 8x8 / 16x16 /
+    24x24 basesWorkers (bench.MIXED), each bucket half selfplay, a quarter vs device
+    workerRushAI, a quarter vs device coacAI -- stepped by one mrts_step_group call with
+    the default merge-fit | bots-first policy (8x8 and 16x16 share one 256-lane launch
+    with a segment table, 24x24 keeps its own), the device Philox sampler on each
+    bucket's eager masks, and bench.preroll's staggered restarts over the first 100 ticks.
+    max_steps 100 over 210 ticks, so every game also reaches its time-limit auto-reset.  One oracle per
+    bucket (ovec_bench_steps: the oracle's identical C sampler + step): raw rewards and
+    dones every tick, the whole obs / mask / source tensors every 10 ticks."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from gym_microrts import _native, microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
+    from oracle_py import OracleVecEnv
+
+    n, seed, max_steps, ticks = 8192, 5, 100, 210
+    buckets, spec = [], []
+    for m, frac in bench.MIXED:
+        nb = int(n * frac) // 4 * 4
+        ais = ["workerRushAI"] * (nb // 4) + ["coacAI"] * (nb // 4)
+        buckets.append(dict(map_paths=[m], num_selfplay_envs=nb // 2, num_bot_envs=len(ais),
+                            ai2s=[getattr(microrts_ai, a) for a in ais]))
+        spec.append((m, nb // 2, ais))
+    assert [b["num_selfplay_envs"] + b["num_bot_envs"] for b in buckets] == [2048, 4096, 2048]
+    env = MicroRTSMixedMapVecEnv(buckets, max_steps=max_steps, return_tensors=True, reward_weight=W,
+                                 obs_dtype=torch.int32)
+    assert env.grouped and env.launch_plan() == ([0, 0, 1], 2)
+    orc = [OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, m)], max_steps=max_steps, ai2s=ais, reward_weight=W)
+           for m, nsp, ais in spec]
+    lib = _native.lib()
+    dev = env.envs[0].device
+    acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=dev) for e in env.envs]
+
+    def same(gpu, host, what, k, s):
+        assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"bucket {k}: {what} differs at tick {s}"
+
+    for k, (og, o) in enumerate(zip(env.reset(), orc)):
+        same(og, o.reset(), "reset obs", k, -1)
+    plans = [bench.stagger_plan(e._n_games(), max_steps) for e in env.envs]
+    ends = np.zeros(3, int)
+    for s in range(ticks):
+        masks = env.get_action_mask()
+        for e, mk, a in zip(env.envs, masks, acts):
+            _native.check(bench.sample(lib, "src", mk, e.source_unit_mask, e.num_envs, e.height * e.width, 0, seed, s, a),
+                          None, "sample")
+        obs, rew, done, infos = env.step(acts)
+        for k, (e, o) in enumerate(zip(env.envs, orc)):
+            _, ro, do = o.bench_steps(1, seed, s)
+            same(infos[k]._raw, ro, "raw rewards", k, s)
+            same(e._done, do.astype(np.uint8), "dones", k, s)
+            assert np.allclose(rew[k].cpu().numpy(), ro @ W, rtol=0, atol=1e-12), f"bucket {k}: reward at tick {s}"
+            ends[k] += int(do[:, 0].sum())
+        if s < max_steps:   # bench.preroll's staggered restarts
+            for e, o, plan in zip(env.envs, orc, plans):
+                e.reset_games(plan[s])
+                for g in plan[s]:
+                    o.reset_game(g, 0)
+        if s % 10 == 0 or s == ticks - 1:
+            for k, (e, o) in enumerate(zip(env.envs, orc)):
+                same(obs[k], o.encode(o.raw_obs()), "obs", k, s)
+                full = o.get_action_mask_full()
+                same(e.get_action_mask(), full[:, :, 1:], "mask", k, s)
+                same(e.source_unit_mask, full[:, :, 0], "source", k, s)
+                del full
+    for k, e in enumerate(env.envs):
+        st = e.game_stats()
+        assert (st[:, 5] >= 1).all(), f"bucket {k}: a game never finished an episode in the window"
+        assert ends[k] >= e.num_envs
+    assert env.error_flags() == 0
+    env.close()
+    for o in orc:
+        o.close()

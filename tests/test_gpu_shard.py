@@ -103,41 +103,46 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("launcher", ["torchrun", "self"])
-def test_bench_sharding_end_to_end(tmp_path, launcher):
-    """bench.py --gpus 2 (2 ranks, gloo) dumps each rank's final outputs; they are the
-    two halves of a 1-rank bench.py run of twice the envs (same seed, staggered
-    pre-roll, warmup and timed steps).  launcher = torchrun: under
-    torch.distributed.run; self: a plain `bench.py --gpus 2`, which starts its two
-    ranks itself (bench.launch_ranks) -- the driver's SCALE invocation."""
+@pytest.mark.parametrize("launcher,world", [("torchrun", 2), ("self", 2), ("self", 4)])
+def test_bench_sharding_end_to_end(tmp_path, launcher, world):
+    """bench.py --gpus N (N ranks, the default gloo timing group) dumps each rank's final
+    outputs; they are the N slices of a 1-rank bench.py run of all the envs (same seed,
+    staggered pre-roll, warmup and timed steps).  launcher = torchrun: under
+    torch.distributed.run (the driver's SCALE invocation); self: a plain
+    `bench.py --gpus N`, which starts its ranks itself (bench.launch_ranks).  The line
+    carries one per-rank entry per rank (window.per_rank)."""
+    total = 512
     common = ["--steps", "25", "--warmup", "3", "--preroll", "120", "--max-steps", "120", "--no-cpu-baseline",
-              "--roofline-steps", "8"]
+              "--roofline-steps", "8", "--rank-timeout", "240"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     bench = os.path.join(REPO, "bench.py")
-    two_args = ["--gpus", "2", "--envs-per-gpu", "256", "--dist-backend", "gloo", "--dump", str(tmp_path / "two")] + common
+    n_args = ["--gpus", str(world), "--envs-per-gpu", str(total // world), "--dump", str(tmp_path / "n")] + common
     if launcher == "torchrun":
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-               "127.0.0.1", "--master-port", str(_free_port()), bench] + two_args
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world), "--master-addr",
+               "127.0.0.1", "--master-port", str(_free_port()), bench] + n_args
     else:
-        cmd = [sys.executable, bench] + two_args
-    two = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
-    assert two.returncode == 0, two.stderr[-3000:]
-    one = subprocess.run([sys.executable, bench, "--envs-per-gpu", "512", "--dump", str(tmp_path / "one")]
+        cmd = [sys.executable, bench] + n_args
+    many = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=270)
+    assert many.returncode == 0, many.stderr[-3000:]
+    one = subprocess.run([sys.executable, bench, "--envs-per-gpu", str(total), "--dump", str(tmp_path / "one")]
                          + common, env=env, capture_output=True, text=True, timeout=240)
     assert one.returncode == 0, one.stderr[-3000:]
     import json
 
-    lines = [ln for ln in two.stdout.strip().splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, two.stdout[-3000:]   # rank 0 only
+    lines = [ln for ln in many.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, many.stdout[-3000:]   # rank 0 only
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["window"]["auto_resets"] > 0
-    assert line["process_group"]["world_size"] == 2 and line["process_group"]["backend"] == "gloo"
+    assert line["n_gpus"] == world and line["window"]["auto_resets"] > 0
+    assert line["process_group"]["world_size"] == world and line["process_group"]["backend"] == "gloo"
     assert ("self" in line["process_group"]["launcher"]) == (launcher == "self")
     assert line["roofline"]["samples"] == 8
+    pr = line["window"]["per_rank"]
+    assert [p["rank"] for p in pr] == list(range(world)) and all(p["env_steps_per_s"] > 0 for p in pr)
+    assert max(p["elapsed_s"] for p in pr) * 1e3 / 25 == pytest.approx(line["ms_per_step"], rel=1e-3)
     whole = np.load(tmp_path / "one.rank0.npz")
-    parts = [np.load(tmp_path / f"two.rank{r}.npz") for r in range(2)]
+    parts = [np.load(tmp_path / f"n.rank{r}.npz") for r in range(world)]
     for k in ("obs", "mask", "src", "raw", "done", "stats"):
         np.testing.assert_array_equal(whole[k], np.concatenate([p[k] for p in parts]), err_msg=k)
 
