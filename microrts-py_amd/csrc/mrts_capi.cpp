@@ -703,7 +703,7 @@ int mrts_sample_actions(void *stream, const int32_t *mask, int32_t n, int32_t hw
 int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t n, int32_t hw, int32_t env0,
                             uint64_t seed, uint32_t step, int64_t *actions) {
     if (!mask || !source || !actions || n < 0 || hw <= 0 || env0 < 0) return MRTS_EINVAL;
-    if ((int64_t)n * hw > (int64_t)INT32_MAX - 64) return MRTS_EINVAL;   // k_sample_src indexes rows in 32 bits
+    if ((int64_t)n * hw > (int64_t)INT32_MAX - 256) return MRTS_EINVAL;   // k_sample_src indexes rows in 32 bits
     return mrts_engine_sample_src(mask, source, n, hw, env0, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
 }
 

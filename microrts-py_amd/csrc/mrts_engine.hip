@@ -1659,17 +1659,13 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restric
 // unit of the player: UnitAction.getValidActionArray is all zero), so only the
 // mask rows of source cells are read -- a few per cent of the 78-channel rows
 // on basesWorkers -- while every row's 7 components are still drawn and
-// written.  One wave per 64 consecutive rows, in two passes:
-//  1. write first: every row's draw as a row without valid entries (uniform over
-//     each component; a function of the Philox words alone, so no load precedes
-//     it) goes out as coalesced 16-B stores right away -- the 117 MB action
-//     stream starts at the kernel's first instruction instead of after two
-//     dependent round trips (source word, then mask rows);
-//  2. patch the source rows (~2 %): the wave loads them cooperatively (channel k
-//     on lane k, two coalesced loads per row, SRC_ROWS rows in flight), folds each
-//     with two ballots, and the row's lane rewrites its 56 B once every store of
-//     pass 1 has completed (s_waitcnt 0: a later store to the same address from
-//     another lane is then ordered after it at the L2).
+// written.  One wave per 64 consecutive rows: the wave reads the rows of its
+// active lanes cooperatively (channel k on lane k, two coalesced loads per row,
+// up to SRC_ROWS (4) rows in flight) and folds each with two ballots.  Measured
+// and refuted in round 5 (profiles/r05_ab/): writing every row's no-valid-entry
+// draw first and patching the source rows after (sampler 32.6 -> 35.6 us, and the
+// next k_step +8 us); two 64-row groups per wave sharing one chain of round trips
+// (32.7 -> 32.4 us, configs[1] 2 % slower).
 constexpr int SR_WAVES = 4;
 constexpr int SRC_ROWS = 4;   // source rows per round trip (8 and 16 measured slower, profiles/r04_ab/r04v)
 __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n,
@@ -1682,14 +1678,41 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
     if (row0 >= rows) return;
     const int rb = (int)min(64ll, rows - row0);
     const bool in = lane < rb;
-    // issued first, waited for after pass 1's stores (tail lanes re-read the last row)
+    // unconditional load (tail lanes re-read the last row): no branch around it, so
+    // its wait falls after the row's Philox words, which are drawn while the source
+    // word (and then the mask rows) are in flight
     const int s_raw = src[row0 + min(lane, rb - 1)];
     uint32_t r8[8];
     const unsigned idx = (unsigned)(row0 + lane);   // rows = n * hw < 2^31 (mrts_sample_actions_src checks)
     const int e = (int)(idx / (unsigned)hw), c = (int)(idx - (unsigned)e * (unsigned)hw);
     philox_row(env0 + e, c, seed, step, r8);
-    // pass 1: every row as a row without valid entries
-    select_row(0, 0, r8, s_out[w] + lane * 7);
+#pragma unroll
+    for (int k = 0; k < 8; k++) asm volatile("" : "+v"(r8[k]));   // computed here, not sunk to their use after the loads
+    const int s = in ? s_raw : 0;
+    uint64_t pending = __ballot(s != 0);
+    uint64_t lo = 0, hi = 0;   // this lane's row as 78 bits
+    while (pending) {          // wave-uniform; SRC_ROWS source rows per round trip
+        int r[SRC_ROWS];
+#pragma unroll
+        for (int k = 0; k < SRC_ROWS; k++) {
+            r[k] = pending ? __builtin_ctzll(pending) : r[0];   // repeats r[0]
+            pending &= pending - 1ull;
+        }
+        int v0[SRC_ROWS], v1[SRC_ROWS];
+#pragma unroll
+        for (int k = 0; k < SRC_ROWS; k++) {   // all the loads in flight before the first ballot
+            const int32_t* m = mask + (row0 + r[k]) * MRTS_MASK_CH;   // (a repeated row re-reads the same bits)
+            v0[k] = __builtin_nontemporal_load(m + lane);
+            v1[k] = __builtin_nontemporal_load(m + 64 + min(lane, MRTS_MASK_CH - 65));
+        }
+#pragma unroll
+        for (int k = 0; k < SRC_ROWS; k++) {
+            const uint64_t b0 = __ballot(v0[k] != 0);
+            const uint64_t b1 = __ballot(lane < MRTS_MASK_CH - 64 && v1[k] != 0);
+            if (lane == r[k]) { lo = b0; hi = b1; }
+        }
+    }
+    if (in) select_row(lo, hi, r8, s_out[w] + lane * 7);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int64_t* ob = act + row0 * 7;   // 16-B aligned: 64 * 56 B per wave
     const int onel = rb * 7, onv = onel >> 1;
@@ -1701,40 +1724,6 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
         __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(o4 + k));
     }
     if ((onel & 1) && lane == 0) ob[onel - 1] = s_out[w][onel - 1];
-    // pass 2: the source rows
-    const int s = in ? s_raw : 0;
-    uint64_t pending = __ballot(s != 0);
-    if (!pending) return;   // wave-uniform
-    uint64_t lo = 0, hi = 0;   // this lane's row as 78 bits
-    while (pending) {          // wave-uniform; SRC_ROWS source rows per round trip
-        int r[SRC_ROWS];
-#pragma unroll
-        for (int k = 0; k < SRC_ROWS; k++) {
-            r[k] = pending ? __builtin_ctzll(pending) : r[0];   // repeats r[0] (same row, same bits)
-            pending &= pending - 1ull;
-        }
-        int v0[SRC_ROWS], v1[SRC_ROWS];
-#pragma unroll
-        for (int k = 0; k < SRC_ROWS; k++) {   // all the loads in flight before the first ballot
-            const int32_t* m = mask + (row0 + r[k]) * MRTS_MASK_CH;
-            v0[k] = __builtin_nontemporal_load(m + lane);
-            v1[k] = __builtin_nontemporal_load(m + 64 + min(lane, MRTS_MASK_CH - 65));
-        }
-#pragma unroll
-        for (int k = 0; k < SRC_ROWS; k++) {
-            const uint64_t b0 = __ballot(v0[k] != 0);
-            const uint64_t b1 = __ballot(lane < MRTS_MASK_CH - 64 && v1[k] != 0);
-            if (lane == r[k]) { lo = b0; hi = b1; }
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0);   // pass 1's stores have completed (vmcnt counts stores on gfx9)
-    if (s) {
-        int64_t out[7];
-        select_row(lo, hi, r8, out);
-        int64_t* o = act + (row0 + lane) * 7;
-#pragma unroll
-        for (int k = 0; k < 7; k++) o[k] = out[k];
-    }
 }
 
 // ---------------------------------------------------------------------------

@@ -98,7 +98,7 @@ def test_checkpoint_same_shape_other_config_refused(what):
     if what == "bots":
         other = _env(n=32, bots=[microrts_ai.workerRushAI] * 16)
     elif what == "map":
-        other = _env(n=32, map_path="maps/16x16/basesWorkers16x16A.xml")
+        other = _env(n=32, map_path="maps/16x16/basesWorkers16x16B.xml")   # (16x16A is byte-identical to 16x16)
     else:
         other = _env(n=32, partial_obs=True)
     env.reset()

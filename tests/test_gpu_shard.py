@@ -140,7 +140,7 @@ def test_bench_sharding_end_to_end(tmp_path, launcher, world):
     assert line["roofline"]["samples"] == 8
     pr = line["window"]["per_rank"]
     assert [p["rank"] for p in pr] == list(range(world)) and all(p["env_steps_per_s"] > 0 for p in pr)
-    assert max(p["elapsed_s"] for p in pr) * 1e3 / 25 == pytest.approx(line["ms_per_step"], rel=1e-3)
+    assert max(p["elapsed_s"] for p in pr) * 1e3 / 25 == pytest.approx(line["ms_per_step"], abs=2e-4)   # 4-decimal line
     whole = np.load(tmp_path / "one.rank0.npz")
     parts = [np.load(tmp_path / f"n.rank{r}.npz") for r in range(world)]
     for k in ("obs", "mask", "src", "raw", "done", "stats"):
