@@ -391,37 +391,165 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
 // res0 / res1: the players' resources (the masks' produce checks), read by the
 // caller from L.sc before the early bot may overwrite the step's scalars.
 template <int NT, int P, typename OT>
+__device__ __forceinline__ void onehot_words(const EngineParams& p, const Lds& L, const Game& G, int c) {
+    const int HW = p.HW, nw = HW / 32 + 1;
+    const uint32_t u = L.unit[c], a = L.act[c];
+    const uint8_t wl = L.wall[c];
+    for (int v = 0; v < G.nviews; v++) {
+        if (P == 31) {
+            const bool shown = u == 0 || u_owner(u) == v || ((L.vis[v * nw + (c >> 5)] >> (c & 31)) & 1u);
+            const bool opp = (L.vis[(1 - v) * nw + (c >> 5)] >> (c & 31)) & 1u;
+            L.outw[v * HW + c] = cell_onehot(u, a, wl, v, P, shown, opp);
+        } else {
+            L.outw[v * HW + c] = cell_onehot(u, a, wl, v);
+        }
+    }
+}
+__device__ __forceinline__ void mask_words(const EngineParams& p, const Lds& L, const Game& G, int c, int res0, int res1) {
+    const int HW = p.HW;
+    const Grid gd{p.W, p.H, HW};
+    for (int v = 0; v < G.nviews; v++) {
+        uint32_t m[3];
+        cell_mask(gd, c, v, L.unit, L.act, L.wall, v == 0 ? res0 : res1, m);
+        L.outm[3 * (v * HW + c)] = m[0];
+        L.outm[3 * (v * HW + c) + 1] = m[1];
+        L.outm[3 * (v * HW + c) + 2] = m[2];
+        p.src_out[(size_t)(G.env0 + v) * HW + c] = (int32_t)(m[0] & 1u);
+    }
+}
+// phase B's obs rows of every view, lanes t0 .. t0 + nt
+template <int P, typename OT>
+__device__ __forceinline__ void stream_obs(const EngineParams& p, const Lds& L, const Game& G, int t0, int nt) {
+    const int HW = p.HW, NV = G.nviews;
+    const uint32_t* ow = L.outw;
+    OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P;
+    const int total = NV * HW * P;
+    if (((HW * P) & 3) == 0) {   // every env's rows start 16-B aligned
+        constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
+        // elements e .. e+3 are planes pl .. pl+3 of cell c, running on into cell
+        // c+1 past plane P-1: one paired LDS read (cells c, c+1) per 16-B store.
+        // (c+1 past the last cell reads the words behind: never used, as the last
+        // store of the run ends at plane P-1.)  A one-hot word has no bit at or
+        // above P, so (w0 >> pl) | (w1 << (P - pl)) are the window's bits.  (c, pl)
+        // advance by a constant per trip: no division in the loop.
+        // Software-pipelined: the next trip's word pair is read before this trip's
+        // store, so the LDS round trip overlaps the bit work instead of stalling every
+        // trip (a lone workgroup's stream -- the kernel's last round -- is bound by this
+        // loop, not by the store path: scripts/store_rate.hip).  The read-ahead index is
+        // clamped into the word region (its last trip's values are never used).
+        const int dq = 4 * nt / P, dr = 4 * nt - dq * P, cmax = NV * HW - 1;
+        int c = 4 * t0 / P, pl = 4 * t0 - c * P;
+        uint32_t w0 = ow[min(c, cmax)], w1 = ow[min(c, cmax) + 1];
+        for (int k = t0; k < total / 4; k += nt) {
+            int cn = c + dq, pn = pl + dr;
+            if (pn >= P) { pn -= P; cn++; }
+            const int cr = min(cn, cmax);
+            const uint32_t n0 = ow[cr], n1 = ow[cr + 1];
+            const uint32_t bits = (w0 >> pl) | (w1 << (P - pl));
+            st16(out + 4 * k, (bits & 1u) ? ONE : 0, (bits & 2u) ? ONE : 0, (bits & 4u) ? ONE : 0, (bits & 8u) ? ONE : 0);
+            w0 = n0;
+            w1 = n1;
+            c = cn;
+            pl = pn;
+        }
+    } else {
+        for (int e = t0; e < total; e += nt) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
+    }
+}
+// phase B's mask rows of every view, lanes t0 .. t0 + nt
+__device__ __forceinline__ void stream_masks(const EngineParams& p, const Lds& L, const Game& G, int t0, int nt) {
+    const int HW = p.HW, NV = G.nviews;
+    const uint32_t* mw = L.outm;
+    int32_t* out = p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH;
+    const int total = NV * HW * MRTS_MASK_CH;
+    if ((HW & 1) == 0) {   // HW * 78 % 4 == 0: every env's rows start 16-B aligned
+        // elements e .. e+3 are channels ch .. ch+3 of row r = bits ch+1 .. ch+4 of
+        // its 79-bit word (bit 0 = source); e is a multiple of 4 and a row pair
+        // is 156 elements, so ch is even and only ch = 76 runs into row r+1
+        // (channels 76, 77 = bits 77, 78, then bits 1, 2 of the next row, whose
+        // first word is the word after bit 78's).  One paired LDS read per store.
+        // (r, ch) advance by a constant per trip; the ch == 76 fix-up is a select,
+        // not a branch.
+        static_assert(MRTS_MASK_CH == 78, "mask row layout");
+        // (software-pipelined as the obs loop: the next trip's word pair read ahead)
+        const int dq = 4 * nt / MRTS_MASK_CH, dr = 4 * nt - dq * MRTS_MASK_CH, wmax = 3 * NV * HW - 1;
+        int r = 4 * t0 / MRTS_MASK_CH, ch = 4 * t0 - r * MRTS_MASK_CH;
+        int r3 = 3 * r;   // the row's first word
+        int wr = min(r3 + ((ch + 1) >> 5), wmax);
+        uint32_t lo = mw[wr], hi = mw[wr + 1];
+        for (int k = t0; k < total / 4; k += nt) {
+            int r3n = r3 + 3 * dq, chn = ch + dr;
+            if (chn >= MRTS_MASK_CH) { chn -= MRTS_MASK_CH; r3n += 3; }
+            wr = min(r3n + ((chn + 1) >> 5), wmax);
+            const uint32_t nlo = mw[wr], nhi = mw[wr + 1];
+            const int b0 = ch + 1;
+            const uint32_t fun = (uint32_t)((((uint64_t)hi << 32) | lo) >> (b0 & 31));
+            const uint32_t bits = ch == 76 ? ((fun & 3u) | ((hi << 1) & 0xCu)) : fun;
+            st16(out + 4 * k, (int)(bits & 1u), (int)((bits >> 1) & 1u), (int)((bits >> 2) & 1u), (int)((bits >> 3) & 1u));
+            lo = nlo;
+            hi = nhi;
+            r3 = r3n;
+            ch = chn;
+        }
+    } else {
+        for (int e = t0; e < total; e += nt) {
+            const int r = e / MRTS_MASK_CH, b = e % MRTS_MASK_CH + 1;
+            out[e] = (int)((mw[3 * r + (b >> 5)] >> (b & 31)) & 1u);
+        }
+    }
+}
+
+// All outputs of one game once its state is final.  Phase A (lane per cell):
+// every view's one-hot word and, with `masks`, its getMasks(0) 79-bit word
+// (+ the source channel, written straight out) into LDS; one barrier; phase B:
+// the views' obs rows, then their mask rows, streamed with 16-byte stores and no
+// further barrier (the envs of a game are adjacent: a selfplay pair 2k, 2k+1
+// writes one contiguous run).  The words live in the region of the step's
+// scratch lists (resv .. snap), dead by now.
+// `skip`: lanes [0, skip) leave after phase A (the bot-fused k_step's wave 0) and
+// the others stream phase B alone.
+// `early_cnt` (the early-bot k_step): wave 0 is running the bot already, so
+// phase A too runs on lanes [skip, NT) only and its end is a counter the
+// streaming waves meet at in LDS instead of a workgroup barrier.
+// res0 / res1: the players' resources (the masks' produce checks), read by the
+// caller from L.sc before the early bot may overwrite the step's scalars.
+// Masks first (no bot in the workgroup, skip == 0): the mask words (no fog
+// dependency) are built and their 2.5x larger stream issued before the one-hot
+// words (and, under partial observability, the sight disks) are computed, so a
+// game's first bytes leave one phase earlier and the obs words are built while the
+// mask stores drain; one more barrier before the obs stream.
+template <int NT, int P, typename OT>
 __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L, const Game& G, bool obs, bool masks, int res0,
                                              int res1, int skip = 0, int* early_cnt = nullptr) {
-    const int HW = p.HW, NV = G.nviews;
-    uint32_t* ow = L.outw;   // [NV][HW]    one-hot bits
-    uint32_t* mw = L.outm;   // [NV][HW][3] mask bits (bit 0 = source)
-    const Grid gd{p.W, p.H, HW};
+    const int HW = p.HW;
+    if (skip == 0 && obs && masks) {
+        const int nw = HW / 32 + 1;
+        for (int c = threadIdx.x; c < HW; c += NT) mask_words(p, L, G, c, res0, res1);
+        if (P == 31)
+            for (int i = threadIdx.x; i < 2 * nw; i += NT) L.vis[i] = 0;
+        __syncthreads();
+        MRTS_STAMP(8, threadIdx.x == 0);
+        __builtin_amdgcn_s_setprio(0);
+        stream_masks(p, L, G, threadIdx.x, NT);
+        if (P == 31) {   // compute_vis's sight disks (cleared above)
+            for (int c = threadIdx.x; c < HW; c += NT) {
+                const uint32_t u = L.unit[c];
+                const int q = u_owner(u);
+                if (u != 0 && q >= 0) or_sight_disk(L.vis + q * nw, c % p.W, c / p.W, ut_sight(u_type(u)), p.W, p.H);
+            }
+            __syncthreads();
+        }
+        for (int c = threadIdx.x; c < HW; c += NT) onehot_words<NT, P, OT>(p, L, G, c);
+        __syncthreads();
+        stream_obs<P, OT>(p, L, G, threadIdx.x, NT);
+        MRTS_STAMP_MAX(9, (threadIdx.x & 63) == 0);
+        return;
+    }
     if (obs && P == 31) compute_vis<NT>(p, L);
-    const int nw = HW / 32 + 1;
     const int a0 = early_cnt ? skip : 0;   // phase A's first lane
     for (int c = (int)threadIdx.x - a0; c < HW; c += NT - a0) {
-        const uint32_t u = L.unit[c], a = L.act[c];
-        const uint8_t wl = L.wall[c];
-        for (int v = 0; v < NV; v++) {
-            if (obs) {
-                if (P == 31) {
-                    const bool shown = u == 0 || u_owner(u) == v || ((L.vis[v * nw + (c >> 5)] >> (c & 31)) & 1u);
-                    const bool opp = (L.vis[(1 - v) * nw + (c >> 5)] >> (c & 31)) & 1u;
-                    ow[v * HW + c] = cell_onehot(u, a, wl, v, P, shown, opp);
-                } else {
-                    ow[v * HW + c] = cell_onehot(u, a, wl, v);
-                }
-            }
-            if (masks) {
-                uint32_t m[3];
-                cell_mask(gd, c, v, L.unit, L.act, L.wall, v == 0 ? res0 : res1, m);
-                mw[3 * (v * HW + c)] = m[0];
-                mw[3 * (v * HW + c) + 1] = m[1];
-                mw[3 * (v * HW + c) + 2] = m[2];
-                p.src_out[(size_t)(G.env0 + v) * HW + c] = (int32_t)(m[0] & 1u);
-            }
-        }
+        if (obs) onehot_words<NT, P, OT>(p, L, G, c);
+        if (masks) mask_words(p, L, G, c, res0, res1);
     }
     if (early_cnt) {   // the streaming waves' own meeting point (wave 0 never arrives)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -442,80 +570,8 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     MRTS_STAMP(8, (int)threadIdx.x == skip);
     __builtin_amdgcn_s_setprio(0);
     const int t0 = (int)threadIdx.x - skip, nt = NT - skip;
-    if (obs) {
-        OT* out = reinterpret_cast<OT*>(p.obs) + (size_t)G.env0 * HW * P;
-        const int total = NV * HW * P;
-        if (((HW * P) & 3) == 0) {   // every env's rows start 16-B aligned
-            constexpr int ONE = std::is_same<OT, float>::value ? 0x3f800000 : 1;   // 1.0f or 1 as stored bits
-            // elements e .. e+3 are planes pl .. pl+3 of cell c, running on into cell
-            // c+1 past plane P-1: one paired LDS read (cells c, c+1) per 16-B store.
-            // (c+1 past the last cell reads the mask words behind: never used, as
-            // the last store of the run ends at plane P-1.)  A one-hot word has no
-            // bit at or above P, so (w0 >> pl) | (w1 << (P - pl)) are the window's
-            // bits.  (c, pl) advance by a constant per trip: no division in the loop.
-            // Software-pipelined: the next trip's word pair is read before this trip's
-            // store, so the LDS round trip overlaps the bit work instead of stalling every
-            // trip (a lone workgroup's stream -- the kernel's last round -- is bound by this
-            // loop, not by the store path: scripts/store_rate.hip).  The read-ahead index is
-            // clamped into the word region (its last trip's values are never used).
-            const int dq = 4 * nt / P, dr = 4 * nt - dq * P, cmax = NV * HW - 1;
-            int c = 4 * t0 / P, pl = 4 * t0 - c * P;
-            uint32_t w0 = ow[min(c, cmax)], w1 = ow[min(c, cmax) + 1];
-            for (int k = t0; k < total / 4; k += nt) {
-                int cn = c + dq, pn = pl + dr;
-                if (pn >= P) { pn -= P; cn++; }
-                const int cr = min(cn, cmax);
-                const uint32_t n0 = ow[cr], n1 = ow[cr + 1];
-                const uint32_t bits = (w0 >> pl) | (w1 << (P - pl));
-                st16(out + 4 * k, (bits & 1u) ? ONE : 0, (bits & 2u) ? ONE : 0, (bits & 4u) ? ONE : 0, (bits & 8u) ? ONE : 0);
-                w0 = n0;
-                w1 = n1;
-                c = cn;
-                pl = pn;
-            }
-        } else {
-            for (int e = t0; e < total; e += nt) out[e] = (OT)((ow[e / P] >> (e % P)) & 1u);
-        }
-    }
-    if (masks) {
-        int32_t* out = p.mask + (size_t)G.env0 * HW * MRTS_MASK_CH;
-        const int total = NV * HW * MRTS_MASK_CH;
-        if ((HW & 1) == 0) {   // HW * 78 % 4 == 0: every env's rows start 16-B aligned
-            // elements e .. e+3 are channels ch .. ch+3 of row r = bits ch+1 .. ch+4 of
-            // its 79-bit word (bit 0 = source); e is a multiple of 4 and a row pair
-            // is 156 elements, so ch is even and only ch = 76 runs into row r+1
-            // (channels 76, 77 = bits 77, 78, then bits 1, 2 of the next row, whose
-            // first word is the word after bit 78's).  One paired LDS read per store.
-            // (r, ch) advance by a constant per trip; the ch == 76 fix-up is a select,
-            // not a branch.
-            static_assert(MRTS_MASK_CH == 78, "mask row layout");
-            // (software-pipelined as the obs loop: the next trip's word pair read ahead)
-            const int dq = 4 * nt / MRTS_MASK_CH, dr = 4 * nt - dq * MRTS_MASK_CH, wmax = 3 * NV * HW - 1;
-            int r = 4 * t0 / MRTS_MASK_CH, ch = 4 * t0 - r * MRTS_MASK_CH;
-            int r3 = 3 * r;   // the row's first word
-            int wr = min(r3 + ((ch + 1) >> 5), wmax);
-            uint32_t lo = mw[wr], hi = mw[wr + 1];
-            for (int k = t0; k < total / 4; k += nt) {
-                int r3n = r3 + 3 * dq, chn = ch + dr;
-                if (chn >= MRTS_MASK_CH) { chn -= MRTS_MASK_CH; r3n += 3; }
-                wr = min(r3n + ((chn + 1) >> 5), wmax);
-                const uint32_t nlo = mw[wr], nhi = mw[wr + 1];
-                const int b0 = ch + 1;
-                const uint32_t fun = (uint32_t)((((uint64_t)hi << 32) | lo) >> (b0 & 31));
-                const uint32_t bits = ch == 76 ? ((fun & 3u) | ((hi << 1) & 0xCu)) : fun;
-                st16(out + 4 * k, (int)(bits & 1u), (int)((bits >> 1) & 1u), (int)((bits >> 2) & 1u), (int)((bits >> 3) & 1u));
-                lo = nlo;
-                hi = nhi;
-                r3 = r3n;
-                ch = chn;
-            }
-        } else {
-            for (int e = t0; e < total; e += nt) {
-                const int r = e / MRTS_MASK_CH, b = e % MRTS_MASK_CH + 1;
-                out[e] = (int)((mw[3 * r + (b >> 5)] >> (b & 31)) & 1u);
-            }
-        }
-    }
+    if (obs) stream_obs<P, OT>(p, L, G, t0, nt);
+    if (masks) stream_masks(p, L, G, t0, nt);
     MRTS_STAMP_MAX(9, (threadIdx.x & 63) == 0);
 }
 
