@@ -188,6 +188,21 @@ def report(steps, a):
                 last = tt[:, 2:].max(axis=1)
                 g.setdefault("end", []).extend((last - t0) * TICK_US)
                 g.setdefault("logic", []).extend(d(2, 7))
+                # the slowest 2 % of this step's workgroups (by end): their phases, side by side
+                endv = (last - t0) * TICK_US
+                cut = np.percentile(endv, 98)
+                sl = tt[endv >= cut]
+                def ds(i, j):
+                    ok = (sl[:, i] > 0) & (sl[:, j] > 0)
+                    return list((sl[ok, j] - sl[ok, i]) * TICK_US)
+                g.setdefault("slow2_end", []).extend(endv[endv >= cut])
+                g.setdefault("slow2_start", []).extend((sl[:, 2] - t0) * TICK_US)
+                g.setdefault("slow2_logic", []).extend(ds(2, 7))
+                g.setdefault("slow2_bot_setup", []).extend(ds(7, 10))
+                g.setdefault("slow2_behaviours", []).extend(ds(10, 11))
+                g.setdefault("slow2_translate", []).extend(ds(11, 12))
+                g.setdefault("slow2_bot_total", []).extend(ds(7, 13))
+                g.setdefault("slow2_stream", []).extend(ds(8, 9))
     for k, g in sorted(acc.items()):
         row = {}
         for name, v in g.items():
