@@ -40,3 +40,20 @@ def test_released_buffer_is_reused():
     # a different shape under the same key gets its own buffer
     e = pool.d2h("raw", torch.zeros((2, 2), dtype=torch.float64))
     assert e.shape == (2, 2) and e.ctypes.data != ptr
+
+
+def test_map_cycle_counts_and_restores():
+    """vec_env.MapCycle: itertools.cycle semantics (vec_env.py's next_map), with the maps
+    drawn counted so a checkpoint restores the cycling position as an integer (ADVICE r4:
+    copying itertools objects is gone in Python 3.14)."""
+    import itertools
+
+    from gym_microrts.envs.vec_env import MapCycle
+
+    maps = ["a", "b", "c"]
+    mc, ref = MapCycle(maps), itertools.cycle(maps)
+    assert [next(mc) for _ in range(7)] == [next(ref) for _ in range(7)]
+    assert mc.drawn == 7
+    back = MapCycle(maps, mc.drawn)
+    assert [next(back) for _ in range(5)] == [next(mc) for _ in range(5)]
+    assert list(MapCycle([])) == []
