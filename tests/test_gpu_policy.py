@@ -111,3 +111,53 @@ def test_trained_policy_lockstep_matches_oracle():
     assert pol["p0_barracks"] > rnd["p0_barracks"]
     assert pol["p0_raw_reward_sums"]["attack"] > 4 * rnd["p0_raw_reward_sums"]["attack"]
     assert pol["cancel_both"] > 4 * rnd["cancel_both"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("map_path,n,ticks,max_steps", [("maps/8x8/basesWorkers8x8.xml", 64, 600, 300),
+                                                        ("maps/24x24/basesWorkers24x24.xml", 64, 800, 500),
+                                                        ("maps/16x16/basesWorkers16x16.xml", 64, 800, 400)])
+def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps):
+    """The same trained policy (fully convolutional encoder / actor: any map whose sides
+    divide by 4) driving 8x8 / 24x24 / 16x16 games, selfplay and vs every device bot kind
+    (8x8: 128-lane fused launch; 24x24: wide-map decode and the 40 KB fused layout): GPU ==
+    oracle every tick."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv
+    from policy import load_policy, policy_actions
+
+    bots = ["coacAI", "workerRushAI", "lightRushAI", "randomBiasedAI", "POWorkerRush", "passiveAI", "randomAI", "PORangedRush"]
+    ais = (bots * n)[:n]
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=n, num_bot_envs=n, max_steps=max_steps, map_paths=[map_path],
+                               ai2s=[getattr(microrts_ai, a) for a in ais], reward_weight=W, return_tensors=True,
+                               obs_dtype=torch.int32)
+    o = OracleVecEnv(n, n, [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais, reward_weight=W)
+    dev = g.device
+    net = load_policy(dev, h=g.height, w=g.width)
+    gen = torch.Generator(device=dev).manual_seed(5)
+
+    def same(gpu, host, what, s):
+        assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"{what} differs at tick {s}"
+
+    obs = g.reset()
+    same(obs, o.reset(), "reset obs", -1)
+    wins = 0
+    for s in range(ticks):
+        mg, mo = g.get_action_mask(), o.get_action_mask()
+        same(mg, mo, "mask", s)
+        a = policy_actions(net, obs, mg, gen)
+        obs, _, dg, ig = g.step(a)
+        oo, ro, do, io = o.step(a.cpu().numpy())
+        raw = np.array([i["raw_rewards"] for i in io])
+        same(obs, oo, "obs", s)
+        same(ig._raw, raw, "raw rewards", s)
+        same(dg, np.asarray(do, bool), "done", s)
+        wins += int((raw[_p0_envs(n, n), 0] > 0).sum())
+    assert g.error_flags() == 0
+    ev = o.event_counts()
+    assert sum(ev["produced"][0].values()) > 0   # the policy's economy runs on these maps too
+    g.close()
+    o.close()
