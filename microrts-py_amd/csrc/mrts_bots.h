@@ -125,6 +125,10 @@ struct BS {
     int kenemy;     // list index of unit k's closest enemy (-1: none), for the behaviours
     // naa <= 64: abstract action k (both int4 words) in lane k; the LDS list is kept too
     int4 kA, kB;
+#ifdef MRTS_STAMPS
+    // the bot's counters (experiment builds), stamped once at its end (columns 16-19)
+    unsigned long long c_entries, c_searches, c_ticks, c_rounds;   // written once, at the bot's end
+#endif
 };
 
 // one unit of the list, read from the registers (or LDS past 64 units)
@@ -358,7 +362,7 @@ __device__ __forceinline__ void pa_add(BS& S, const BL& L, int c, int code) {
 // Breadth-first layers grow from the goal set (free cells within `range` of
 // the target) over free cells; the first layer that touches a free neighbour
 // of the start decides the move, ties UP, RIGHT, DOWN, LEFT.  -1 = null.
-__device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
+__device__ __forceinline__ int pf_dir_search(const BS& S, int sc, int tx, int ty, int range) {
     const int lane = blane(), sx = sc % S.W, sy = sc / S.W, r2 = range * range;
     if ((sx - tx) * (sx - tx) + (sy - ty) * (sy - ty) <= r2) return -1;
     const uint32_t rowmask = S.W == 32 ? 0xFFFFFFFFu : ((1u << S.W) - 1u);
@@ -396,6 +400,9 @@ __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int r
     // layer at a time (a layer after an empty one is empty too)
     uint32_t seen = goal, front = goal;
     for (int it = 0; it <= S.HW; it += 4) {
+#ifdef MRTS_STAMPS
+        const_cast<BS&>(S).c_rounds++;   // four-layer rounds
+#endif
         const uint32_t g1 = grow_of(front, seen), s1 = seen | g1;
         const uint32_t g2 = grow_of(g1, s1), s2 = s1 | g2;
         const uint32_t g3 = grow_of(g2, s2), s3 = s2 | g3;
@@ -408,6 +415,19 @@ __device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int r
         front = g4;
     }
     return -1;
+}
+
+// (experiment builds: the searches' count and summed time per bot)
+__device__ __forceinline__ int pf_dir(const BS& S, int sc, int tx, int ty, int range) {
+#ifdef MRTS_STAMPS
+    const unsigned long long t0 = wall_clock64();
+    const int d = pf_dir_search(S, sc, tx, ty, range);
+    const_cast<BS&>(S).c_searches++;
+    const_cast<BS&>(S).c_ticks += wall_clock64() - t0;
+    return d;
+#else
+    return pf_dir_search(S, sc, tx, ty, range);
+#endif
 }
 
 // ---- abstract actions ----------------------------------------------------------
@@ -611,6 +631,9 @@ __device__ __forceinline__ void translate_actions_lanes(BS& S, const BL& L) {
         int4 ak = lane_int4(a, k);
         const int4 bk = lane_int4(b, k);
         const int cuk = lane_value(cu, k);
+#ifdef MRTS_STAMPS
+        S.c_entries++;   // executed entries
+#endif
         const int code = aa_execute(S, L, ak, bk, cuk);
         if (code >= 0) {
             RU r = usage(S, cuk, code, S.player);
@@ -1215,6 +1238,9 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     int32_t* genv = p.genv + (size_t)g * MRTS_GENV_WORDS;
     const int w_aa = player ? MRTS_G_AA_N : MRTS_G_AA_N0, w_npa = player ? MRTS_G_NPA : MRTS_G_NPA0;
     BS S;
+#ifdef MRTS_STAMPS
+    S.c_entries = S.c_searches = S.c_ticks = S.c_rounds = 0;
+#endif
     S.ai = player ? p.bot_ai[b] : (p.bot_ai0 ? p.bot_ai0[b] : -1);
     if (S.ai < 0) return;            // the agent plays this side
     if (S.ai == MRTS_AI_PASSIVE) {   // PassiveAI: all NONE (k_step's fill)
@@ -1425,6 +1451,10 @@ __device__ __forceinline__ void bot_game(const EngineParams& p, int b, int playe
     }
     bot_sync<FUSED>();
     if (FUSED) MRTS_STAMP(12, lane == 0);
+    MRTS_STAMP_ADD(16, S.c_entries, FUSED && lane == 0);
+    MRTS_STAMP_ADD(17, S.c_searches, FUSED && lane == 0);
+    MRTS_STAMP_ADD(18, S.c_ticks, FUSED && lane == 0);
+    MRTS_STAMP_ADD(19, S.c_rounds, FUSED && lane == 0);
     for (int i = lane; i < S.npa; i += BT) pa_g[i] = L.pa[i];
     for (int i = lane; i < 2 * S.naa; i += BT) aa_g[i] = L.aa[i];
     if (lane0()) {

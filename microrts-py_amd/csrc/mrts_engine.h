@@ -11,7 +11,7 @@
 // Compiled out of the product library.
 #ifdef MRTS_STAMPS
 #define MRTS_STAMP_ROWS 65536
-#define MRTS_STAMP_COLS 16
+#define MRTS_STAMP_COLS 20   // 2..15 phase stamps, 16..19 bot counters (MRTS_STAMP_ADD)
 static __device__ unsigned long long g_stamp[MRTS_STAMP_ROWS][MRTS_STAMP_COLS];
 __shared__ int mrts_stamp_row;
 // mrts_stamp_row: set by k_step's thread 0 before a barrier; every other kernel
@@ -23,10 +23,14 @@ __shared__ int mrts_stamp_row;
     do { if ((cond) && (unsigned)mrts_stamp_row < (unsigned)MRTS_STAMP_ROWS) \
              atomicMax(&g_stamp[mrts_stamp_row][k], (unsigned long long)wall_clock64()); } while (0)
 #define MRTS_STAMP_NONE() do { if (threadIdx.x == 0) mrts_stamp_row = -1; __syncthreads(); } while (0)
+// a counter of the row (one writer: the bot wave's lane 0)
+#define MRTS_STAMP_ADD(k, v, cond) \
+    do { if ((cond) && (unsigned)mrts_stamp_row < (unsigned)MRTS_STAMP_ROWS) g_stamp[mrts_stamp_row][k] += (v); } while (0)
 #else
 #define MRTS_STAMP(k, cond) do { } while (0)
 #define MRTS_STAMP_MAX(k, cond) do { } while (0)
 #define MRTS_STAMP_NONE() do { } while (0)
+#define MRTS_STAMP_ADD(k, v, cond) do { } while (0)
 #endif
 
 struct EngineParams {

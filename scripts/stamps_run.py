@@ -67,7 +67,7 @@ def main():
         one_step(s)
     torch.cuda.synchronize()
     rows = []
-    buf = np.zeros((65536, 16), np.uint64)
+    buf = np.zeros((65536, 20), np.uint64)
     gap[0] = a.gap_us * 1e-6
     if a.read_mb:
         gap.append(torch.ones(a.read_mb << 18, dtype=torch.float32, device=dev))
@@ -203,6 +203,13 @@ def report(steps, a):
                 g.setdefault("slow2_translate", []).extend(ds(11, 12))
                 g.setdefault("slow2_bot_total", []).extend(ds(7, 13))
                 g.setdefault("slow2_stream", []).extend(ds(8, 9))
+                # bot counters (fused bot games): executed translate entries, path searches,
+                # their summed time (us) and four-layer rounds
+                if r.shape[1] >= 20:
+                    bot = tt[:, 7] > 0
+                    for nm, col, scale in (("entries", 16, 1), ("searches", 17, 1), ("search_us", 18, TICK_US), ("rounds", 19, 1)):
+                        g.setdefault("bot_" + nm, []).extend(tt[bot, col] * scale)
+                        g.setdefault("slow2_bot_" + nm, []).extend(sl[sl[:, 7] > 0, col] * scale)
     for k, g in sorted(acc.items()):
         row = {}
         for name, v in g.items():
