@@ -114,14 +114,16 @@ def test_trained_policy_lockstep_matches_oracle():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("map_path,n,ticks,max_steps", [("maps/8x8/basesWorkers8x8.xml", 64, 600, 300),
-                                                        ("maps/24x24/basesWorkers24x24.xml", 64, 800, 500),
-                                                        ("maps/16x16/basesWorkers16x16.xml", 64, 800, 400)])
-def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps):
+@pytest.mark.parametrize("map_path,n,ticks,max_steps,partial_obs", [("maps/8x8/basesWorkers8x8.xml", 64, 600, 300, False),
+                                                                    ("maps/24x24/basesWorkers24x24.xml", 64, 800, 500, False),
+                                                                    ("maps/16x16/basesWorkers16x16.xml", 64, 800, 400, False),
+                                                                    ("maps/16x16/basesWorkers16x16A.xml", 128, 900, 600, True)])
+def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps, partial_obs):
     """The same trained policy (fully convolutional encoder / actor: any map whose sides
     divide by 4) driving 8x8 / 24x24 / 16x16 games, selfplay and vs every device bot kind
-    (8x8: 128-lane fused launch; 24x24: wide-map decode and the 40 KB fused layout): GPU ==
-    oracle every tick."""
+    (8x8: 128-lane fused launch; 24x24: wide-map decode and the 40 KB fused layout), and
+    under partial observability (the policy reads the first 29 of the 31 planes -- hidden
+    units read as empty cells -- against the fogged bots): GPU == oracle every tick."""
     import torch
 
     from gym_microrts import microrts_ai
@@ -133,8 +135,9 @@ def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps):
     ais = (bots * n)[:n]
     g = MicroRTSGridModeVecEnv(num_selfplay_envs=n, num_bot_envs=n, max_steps=max_steps, map_paths=[map_path],
                                ai2s=[getattr(microrts_ai, a) for a in ais], reward_weight=W, return_tensors=True,
-                               obs_dtype=torch.int32)
-    o = OracleVecEnv(n, n, [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais, reward_weight=W)
+                               obs_dtype=torch.int32, partial_obs=partial_obs)
+    o = OracleVecEnv(n, n, [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais, reward_weight=W,
+                     partial_obs=partial_obs)
     dev = g.device
     net = load_policy(dev, h=g.height, w=g.width)
     gen = torch.Generator(device=dev).manual_seed(5)
@@ -148,7 +151,7 @@ def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps):
     for s in range(ticks):
         mg, mo = g.get_action_mask(), o.get_action_mask()
         same(mg, mo, "mask", s)
-        a = policy_actions(net, obs, mg, gen)
+        a = policy_actions(net, obs[..., :29], mg, gen)
         obs, _, dg, ig = g.step(a)
         oo, ro, do, io = o.step(a.cpu().numpy())
         raw = np.array([i["raw_rewards"] for i in io])
