@@ -9,6 +9,16 @@
 //   mode 2  wave-local cells: wave w writes the obs and mask rows of cells [64w, 64w + 64) of each
 //           view (the order a barrier-free, per-wave phase A / B would produce)
 //   mode 3  grid-stride fill of both buffers (torch fill_'s order; 1792 resident workgroups)
+//   mode 4  as 3 with one constant value in every store (what a fill writes)
+//   mode 5  as 3 with non-temporal stores
+//   mode 6  as 0 (phase B order) with one constant value in every store
+//   mode 7  hipMemsetD32Async of both buffers (the runtime's fill: 256 workgroups of 256 lanes)
+//   mode 8  as 3 on 256 workgroups (one per CU), mode 9 on 512, mode 10 on 1024
+//   mode 11 as 0 (phase B order, 4096 workgroups) with only waves 0-1 storing (128 lanes)
+//   mode 12 as 0 with only wave 0 storing (64 lanes)
+//   mode 13 as 8 (256 workgroups) with non-temporal stores
+//   mode 14 games' runs (phase B order) by 256 persistent workgroups (game b, b + 256, ...)
+//   mode 15 games' runs by 1024 persistent workgroups, mode 16 by 512
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/write_pattern scripts/write_pattern.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -21,14 +31,36 @@ __device__ __forceinline__ void st(int* p, int k, int salt) {
     v4i v = {k ^ salt, k + 1, k + 2, salt};
     *reinterpret_cast<v4i*>(p) = v;
 }
+__device__ __forceinline__ void stc(int* p, int salt) {
+    v4i v = {salt, salt, salt, salt};
+    *reinterpret_cast<v4i*>(p) = v;
+}
+__device__ __forceinline__ void stnt(int* p, int k, int salt) {
+    v4i v = {k ^ salt, k + 1, k + 2, salt};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(p));
+}
 
 __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, int G, int salt) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    if (mode == 3) {
+    if (mode >= 8 && mode <= 10) mode = 3;
+    if (mode == 13) mode = 5;
+    if (mode >= 14 && mode <= 16) {
+        const int no = NV * HW * P / 4, nm = NV * HW * CH / 4;
+        for (int g = blockIdx.x; g < G; g += gridDim.x) {
+            int* o = obs + (size_t)g * NV * HW * P;
+            int* m = mask + (size_t)g * NV * HW * CH;
+            for (int k = t; k < no; k += 256) st(o + 4 * k, k, salt);
+            for (int k = t; k < nm; k += 256) st(m + 4 * k, k, salt);
+        }
+        return;
+    }
+    if (mode == 3 || mode == 4 || mode == 5) {
         const long long nobs = (long long)G * NV * HW * P / 4, nmask = (long long)G * NV * HW * CH / 4;
         const long long stride = (long long)gridDim.x * 256;
-        for (long long k = blockIdx.x * 256ll + t; k < nobs; k += stride) st(obs + 4 * k, (int)k, salt);
-        for (long long k = blockIdx.x * 256ll + t; k < nmask; k += stride) st(mask + 4 * k, (int)k, salt);
+        for (long long k = blockIdx.x * 256ll + t; k < nobs; k += stride)
+            mode == 3 ? st(obs + 4 * k, (int)k, salt) : mode == 4 ? stc(obs + 4 * k, salt) : stnt(obs + 4 * k, (int)k, salt);
+        for (long long k = blockIdx.x * 256ll + t; k < nmask; k += stride)
+            mode == 3 ? st(mask + 4 * k, (int)k, salt) : mode == 4 ? stc(mask + 4 * k, salt) : stnt(mask + 4 * k, (int)k, salt);
         return;
     }
     const int g = blockIdx.x;
@@ -38,6 +70,14 @@ __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, 
     if (mode == 0) {
         for (int k = t; k < no; k += 256) st(o + 4 * k, k, salt);
         for (int k = t; k < nm; k += 256) st(m + 4 * k, k, salt);
+    } else if (mode == 11 || mode == 12) {
+        const int nt = mode == 11 ? 128 : 64;
+        if (t >= nt) return;
+        for (int k = t; k < no; k += nt) st(o + 4 * k, k, salt);
+        for (int k = t; k < nm; k += nt) st(m + 4 * k, k, salt);
+    } else if (mode == 6) {
+        for (int k = t; k < no; k += 256) stc(o + 4 * k, salt);
+        for (int k = t; k < nm; k += 256) stc(m + 4 * k, salt);
     } else if (mode == 1) {
         const int qo = no / 4, qm = nm / 4;
         for (int k = w * qo + l; k < (w + 1) * qo; k += 64) st(o + 4 * k, k, salt);
@@ -61,14 +101,26 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[4] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill"};
+    const char* names[17] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
+                             "grid_stride_constant", "grid_stride_nontemporal", "phaseB_constant", "hipMemsetD32",
+                             "grid_stride_256wg", "grid_stride_512wg", "grid_stride_1024wg", "phaseB_2waves", "phaseB_1wave",
+                             "grid_stride_256wg_nt", "games_256_persistent", "games_1024_persistent", "games_512_persistent"};
+    auto launch = [&](int mode, int grid, int i) {
+        if (mode == 7) {
+            hipMemsetD32Async((hipDeviceptr_t)obs, i, bo / 4, 0);
+            hipMemsetD32Async((hipDeviceptr_t)mask, i, bm / 4, 0);
+        } else {
+            hipLaunchKernelGGL(k_pattern, dim3(grid), dim3(256), 0, 0, mode, obs, mask, G, i);
+        }
+    };
     for (int round = 0; round < 3; round++) {
-        for (int mode = 0; mode < 4; mode++) {
-            const int grid = mode == 3 ? 256 * 7 : G;
-            for (int i = 0; i < 5; i++) hipLaunchKernelGGL(k_pattern, dim3(grid), dim3(256), 0, 0, mode, obs, mask, G, i);
+        for (int mode = 0; mode < 17; mode++) {
+            const int grid = (mode >= 3 && mode <= 5) ? 256 * 7 : (mode == 8 || mode == 13 || mode == 14) ? 256
+                           : (mode == 9 || mode == 16) ? 512 : (mode == 10 || mode == 15) ? 1024 : G;
+            for (int i = 0; i < 5; i++) launch(mode, grid, i);
             hipEventRecord(a);
             const int it = 50;
-            for (int i = 0; i < it; i++) hipLaunchKernelGGL(k_pattern, dim3(grid), dim3(256), 0, 0, mode, obs, mask, G, i);
+            for (int i = 0; i < it; i++) launch(mode, grid, i);
             hipEventRecord(b);
             hipEventSynchronize(b);
             float ms = 0;
