@@ -41,6 +41,11 @@ from gym_microrts import _native
 from gym_microrts._native import MicroRTSError, MicroRTSNotImplemented
 from gym_microrts._spaces import Box, Discrete, MultiDiscrete
 
+# Tracing: MICRORTS_AMD_MARKERS=1 puts a named roctx range ("mrts_step",
+# "mrts_masks", "mrts_reset", ...) around every engine launch, for rocprofv3 --marker-trace /
+# --sys-trace timelines next to the kernel trace; off by default (no call at all)
+MARKERS = os.environ.get("MICRORTS_AMD_MARKERS", "0").strip() not in ("", "0")
+
 RENDER_SIZE = 640   # vec_env.py:1083: Image.frombytes("RGB", (640, 640), ...)
 
 RF_NAMES = [
@@ -353,6 +358,8 @@ class MicroRTSGridModeVecEnv:
 
     def _launch(self, name, fn, *args):
         ev = self.kernel_events
+        if MARKERS:   # a named host range around the C-ABI call (rocprofv3 --marker-trace)
+            torch.cuda.nvtx.range_push(f"mrts_{name}")
         if ev is None:
             rc = fn(*args)
         else:
@@ -361,6 +368,8 @@ class MicroRTSGridModeVecEnv:
             rc = fn(*args)
             e.record()
             ev.setdefault(name, []).append((s, e))
+        if MARKERS:
+            torch.cuda.nvtx.range_pop()
         _native.check(rc, self._h, name)
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
