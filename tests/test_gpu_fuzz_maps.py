@@ -1,0 +1,35 @@
+"""Random-map fuzzing of GPU == oracle (tests/random_maps.py): map sizes 4..32 x 4..32, wall
+density 0-25 %, 4 to 200 units of every type, random starting resources, a random mix of
+device bots, selfplay pairs, full or partial observability, random time limits, masked and
+unmasked agent actions.  MRTS_FUZZ_SEEDS / MRTS_FUZZ_FIRST set the number of cases and the
+first seed (default 12 from 0; the round-5 campaign ran seeds 0-2199, profiles/r05_fuzz/)."""
+import os
+
+import numpy as np
+import pytest
+
+from random_maps import write_random_map
+from test_gpu_bots import BOTS, lockstep
+
+pytestmark = pytest.mark.gpu
+SEEDS = int(os.environ.get("MRTS_FUZZ_SEEDS", "12"))
+FIRST = int(os.environ.get("MRTS_FUZZ_FIRST", "0"))
+
+
+def case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    w, h = int(rng.integers(4, 33)), int(rng.integers(4, 33))
+    n = int(rng.integers(4, max(5, min(200, int(w * h * 0.6)))))
+    bots = [str(b) for b in rng.choice(BOTS + ["passiveAI"], size=int(rng.integers(0, 9)))]
+    return dict(w=w, h=h, n=n, walls=float(rng.uniform(0, 0.25)), res=(int(rng.integers(0, 30)), int(rng.integers(0, 30))),
+                bots=bots, nsp=2 * int(rng.integers(0 if bots else 1, 4)), partial=bool(rng.integers(0, 2)),
+                max_steps=int(rng.integers(30, 200)))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", range(FIRST, FIRST + SEEDS))
+def test_fuzz_map_lockstep(tmp_path, seed):
+    c = case(seed)
+    path = write_random_map(str(tmp_path / f"fuzz{seed}.xml"), c["w"], c["h"], seed, n_units=min(c["n"], c["w"] * c["h"] - 4),
+                            wall_frac=c["walls"], res=c["res"])
+    lockstep(c["bots"], path, c["nsp"], 160, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed")
