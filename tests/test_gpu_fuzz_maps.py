@@ -2,7 +2,8 @@
 density 0-25 %, 4 to 200 units of every type, random starting resources, a random mix of
 device bots, selfplay pairs, full or partial observability, random time limits, masked and
 unmasked agent actions.  MRTS_FUZZ_SEEDS / MRTS_FUZZ_FIRST set the number of cases and the
-first seed (default 12 from 0; the round-5 campaign ran seeds 0-2199, profiles/r05_fuzz/)."""
+first seed (default 12 from 0; the round-5 campaign ran seeds 0-2199 of the single-engine
+cases and 0-1499 of the grouped-launch cases, profiles/r05_fuzz/)."""
 import os
 
 import numpy as np
@@ -33,3 +34,35 @@ def test_fuzz_map_lockstep(tmp_path, seed):
     path = write_random_map(str(tmp_path / f"fuzz{seed}.xml"), c["w"], c["h"], seed, n_units=min(c["n"], c["w"] * c["h"] - 4),
                             wall_frac=c["walls"], res=c["res"])
     lockstep(c["bots"], path, c["nsp"], 160, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed")
+
+
+def group_case(seed):
+    rng = np.random.default_rng(5000 + seed)
+    nb = int(rng.integers(2, 5))
+    sizes, spec = set(), []
+    while len(sizes) < nb:
+        sizes.add((int(rng.integers(4, 33)), int(rng.integers(4, 33))))
+    for k, (w, h) in enumerate(sorted(sizes)):
+        bots = [str(b) for b in rng.choice(BOTS + ["passiveAI"], size=int(rng.integers(0, 5)))]
+        spec.append(dict(w=w, h=h, n=int(rng.integers(4, max(5, min(120, int(w * h * 0.5))))), walls=float(rng.uniform(0, 0.2)),
+                         bots=bots, nsp=2 * int(rng.integers(0 if bots else 1, 3))))
+    policy = [0, 1, 2, 1 | 4, 2 | 4][int(rng.integers(0, 5))]
+    return spec, policy, bool(rng.integers(0, 2)), int(rng.integers(30, 150))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", range(FIRST, FIRST + max(1, SEEDS // 3)))
+def test_fuzz_step_group_lockstep(tmp_path, seed):
+    """mrts_step_group over 2-4 random map sizes (each its own engine) under every grouping
+    policy -- separate launches, merge-fit, merge-all, bots first -- so maps of any size share
+    a workgroup width and a segment table with others: every bucket == its own oracle."""
+    from test_gpu_bots import mixed_lockstep
+
+    spec, policy, partial, max_steps = group_case(seed)
+    rows = []
+    for k, c in enumerate(spec):
+        path = write_random_map(str(tmp_path / f"g{seed}_{k}.xml"), c["w"], c["h"], seed * 10 + k,
+                                n_units=min(c["n"], c["w"] * c["h"] - 4), wall_frac=c["walls"])
+        rows.append((path, c["nsp"], c["bots"]))
+    env = mixed_lockstep(rows, 120, max_steps=max_steps, partial_obs=partial, group_policy=policy)
+    assert env.grouped
