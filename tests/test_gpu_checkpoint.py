@@ -5,6 +5,7 @@ sources, raw rewards and dones every step -- with device bots deciding (fused an
 not), partial observability, time-limit resets inside the replayed stretch, and map
 cycling.  A snapshot of another configuration is refused."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -113,3 +114,47 @@ def test_checkpoint_same_shape_other_config_refused(what):
     env.set_state(snap)   # its own snapshot still loads
     env.close()
     other.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MRTS_FUZZ_FIRST", "0")),
+                                       int(os.environ.get("MRTS_FUZZ_FIRST", "0")) + max(1, int(os.environ.get("MRTS_FUZZ_SEEDS", "12")) // 3)))
+def test_fuzz_checkpoint_replays_bit_for_bit(tmp_path, seed):
+    """Random maps (tests/random_maps.py, 4..32 x 4..32, walls), random device bots
+    (randomBiasedAI's tick-keyed stream included), selfplay, fog, map cycling over two random
+    maps of one size, short time limits: the snapshot taken at a random tick replays a random
+    continuation bit for bit (MRTS_FUZZ_SEEDS // 3 cases)."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from random_maps import write_random_map
+    from test_gpu_bots import BOTS
+
+    rng = np.random.default_rng(7000 + seed)
+    w, h = int(rng.integers(4, 33)), int(rng.integers(4, 33))
+    maps = [write_random_map(str(tmp_path / f"k{seed}_{j}.xml"), w, h, seed * 10 + j,
+                             n_units=min(int(rng.integers(4, max(5, min(120, int(w * h * 0.5))))), w * h - 4),
+                             wall_frac=float(rng.uniform(0, 0.2))) for j in range(2)]
+    bots = [str(b) for b in rng.choice(BOTS + ["passiveAI"], size=int(rng.integers(0, 9)))]
+    nsp = 2 * int(rng.integers(0 if bots else 1, 5))
+    kw = dict(cycle_maps=maps) if rng.integers(0, 2) else {}
+    env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=len(bots), max_steps=int(rng.integers(20, 80)),
+                                 ai2s=[getattr(microrts_ai, b) for b in bots], map_paths=[maps[0]],
+                                 partial_obs=bool(rng.integers(0, 2)), reward_weight=W, return_tensors=True,
+                                 obs_dtype=torch.int32, bot_fusion=bool(rng.integers(0, 4)), **kw)
+    env.reset()
+    act = torch.empty((env.num_envs, env.height * env.width, 7), dtype=torch.int64, device=env.device)
+    t0, t1 = int(rng.integers(0, 120)), int(rng.integers(1, 120))
+    first = _run(env, 0, t0, act)
+    state = env.get_state()
+    a = _run(env, t0, t1, act)
+    obs_back = env.set_state(state)
+    if first:
+        assert torch.equal(obs_back, first[-1][2])
+    b = _run(env, t0, t1, act)
+    for s, (x, y) in enumerate(zip(a, b)):
+        for k in range(5):
+            assert torch.equal(x[k], y[k]), f"step {t0 + s} output {k}"
+    assert env.error_flags() == 0
+    env.close()
