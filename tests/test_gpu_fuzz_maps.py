@@ -66,3 +66,42 @@ def test_fuzz_step_group_lockstep(tmp_path, seed):
         rows.append((path, c["nsp"], c["bots"]))
     env = mixed_lockstep(rows, 120, max_steps=max_steps, partial_obs=partial, group_policy=policy)
     assert env.grouped
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", range(FIRST, FIRST + max(1, SEEDS // 3)))
+def test_fuzz_bot_vs_bot_lockstep(tmp_path, seed):
+    """MicroRTSBotVecEnv (vec_env.py:1104-1236) on random maps: random device bots on both sides
+    (k_bot for player 0 and the fused bot for player 1), fog, random time limits; raw rewards,
+    dones and obs == the oracle's every tick."""
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSBotVecEnv
+    from oracle_py import OracleVecEnv
+
+    rng = np.random.default_rng(3000 + seed)
+    w, h = int(rng.integers(4, 33)), int(rng.integers(4, 33))
+    n = int(rng.integers(4, max(5, min(200, int(w * h * 0.6)))))
+    path = write_random_map(str(tmp_path / f"b{seed}.xml"), w, h, seed, n_units=min(n, w * h - 4),
+                            wall_frac=float(rng.uniform(0, 0.25)), res=(int(rng.integers(0, 30)), int(rng.integers(0, 30))))
+    k = int(rng.integers(1, 9))
+    ai1 = [str(b) for b in rng.choice(BOTS + ["passiveAI"], size=k)]
+    ai2 = [str(b) for b in rng.choice(BOTS + ["passiveAI"], size=k)]
+    partial, max_steps = bool(rng.integers(0, 2)), int(rng.integers(30, 200))
+    rw = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    g = MicroRTSBotVecEnv(ai1s=[getattr(microrts_ai, a) for a in ai1], ai2s=[getattr(microrts_ai, a) for a in ai2],
+                          map_paths=[path], max_steps=max_steps, partial_obs=partial, reward_weight=rw)
+    o = OracleVecEnv(0, k, [path], max_steps=max_steps, ai2s=ai2, ai1s=ai1, partial_obs=partial, reward_weight=rw)
+    g.reset()
+    o.reset()
+    hw = g.height * g.width
+    for s in range(160):
+        _, rg, dg, ig = g.step(np.zeros((k, hw * 7), np.int64))
+        o.source_unit_mask = np.zeros((k, hw), np.int32)
+        ro, do = o.step_raw(np.zeros((k, hw, 7), np.int64))
+        np.testing.assert_array_equal(np.array([i["raw_rewards"] for i in ig]), ro, err_msg=f"step {s}")
+        np.testing.assert_array_equal(dg, do[:, 0])
+        np.testing.assert_array_equal(rg, ro @ rw)
+        np.testing.assert_array_equal(g._obs.cpu().numpy().astype(np.int32), o.encode(o.raw_obs()), err_msg=f"obs {s}")
+    assert g.error_flags() == 0
+    g.close()
+    o.close()
