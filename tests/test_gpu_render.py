@@ -91,3 +91,35 @@ def test_hello_world_example_runs():
         np.testing.assert_array_equal(reward, ro)
         np.testing.assert_array_equal(done, do)
     o.close()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MRTS_FUZZ_FIRST", "0")),
+                                       int(os.environ.get("MRTS_FUZZ_FIRST", "0")) + max(1, int(os.environ.get("MRTS_FUZZ_SEEDS", "12")) // 3)))
+def test_fuzz_rgb_array_random_maps(tmp_path, seed):
+    """Frames of random maps (tests/random_maps.py: 4..32 x 4..32, so the cell size, the
+    centring margins and non-square boards vary; walls; every unit type; actions in flight)
+    == oracle_py.render_frame pixel for pixel."""
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv, parse_map, render_frame, sample_actions
+    from random_maps import write_random_map
+
+    rng = np.random.default_rng(11000 + seed)
+    w, h = int(rng.integers(4, 33)), int(rng.integers(4, 33))
+    path = write_random_map(str(tmp_path / f"r{seed}.xml"), w, h, seed,
+                            n_units=min(int(rng.integers(4, max(5, min(150, int(w * h * 0.6))))), w * h - 4),
+                            wall_frac=float(rng.uniform(0, 0.25)))
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=2, num_bot_envs=0, max_steps=60, map_paths=[path])
+    o = OracleVecEnv(2, 0, [path], max_steps=60)
+    wall = parse_map(path)["terrain"]
+    g.reset()
+    o.reset()
+    for s in range(80):
+        if s % 8 == 0:
+            np.testing.assert_array_equal(g.render("rgb_array"), render_frame(o.dump_cells(0), wall, g.width, g.height),
+                                          err_msg=f"{w}x{h} frame at step {s}")
+        m = o.get_action_mask()
+        a = sample_actions(m, seed, s)
+        g.step(a)
+        o.step(a)
+    g.close()
+    o.close()
