@@ -927,6 +927,16 @@ class MicroRTSMixedMapVecEnv:
             f |= e.error_flags()
         return f
 
+    def get_state(self):
+        """Env-state checkpoint of every bucket (MicroRTSGridModeVecEnv.get_state, in bucket order)."""
+        return [e.get_state() for e in self.envs]
+
+    def set_state(self, states):
+        """Restore a get_state() list of this env; returns the restored obs per bucket."""
+        if len(states) != len(self.envs):
+            raise ValueError(f"set_state expects {len(self.envs)} bucket states, got {len(states)}")
+        return [e.set_state(st) for e, st in zip(self.envs, states)]
+
     def close(self):
         for e in self.envs:
             e.close()
@@ -1055,6 +1065,28 @@ class MicroRTSSizeCyclingVecEnv:
             f |= e.error_flags()
         return f
 
+    def get_state(self):
+        """Env-state checkpoint: every size engine's snapshot (its played and parked games),
+        the size each env plays in and the cycle position."""
+        return SizeCyclingState([e.get_state() for e in self.envs], self.bucket.copy(), self.next_map.drawn)
+
+    def set_state(self, state):
+        """Restore a get_state() snapshot of this env; returns the restored obs per size."""
+        if not isinstance(state, SizeCyclingState) or len(state.engines) != len(self.envs):
+            raise ValueError("set_state expects a SizeCyclingState returned by get_state() of this env")
+        out = [e.set_state(st) for e, st in zip(self.envs, state.engines)]
+        self.bucket = state.bucket.copy()
+        self.next_map = MapCycle(self.cycle_maps, state.drawn)
+        return out
+
     def close(self):
         for e in self.envs:
             e.close()
+
+
+class SizeCyclingState:
+    """MicroRTSSizeCyclingVecEnv.get_state: one EnvState per size engine, the env -> size
+    index map and the maps drawn from cycle_maps so far."""
+
+    def __init__(self, engines, bucket, drawn):
+        self.engines, self.bucket, self.drawn = engines, bucket, drawn

@@ -158,3 +158,95 @@ def test_fuzz_checkpoint_replays_bit_for_bit(tmp_path, seed):
             assert torch.equal(x[k], y[k]), f"step {t0 + s} output {k}"
     assert env.error_flags() == 0
     env.close()
+
+
+def _run_multi(env, s0, steps, acts):
+    """_run for the per-bucket / per-size envs: device sampler on every engine, outputs cloned."""
+    import torch
+
+    from gym_microrts import _native
+
+    lib, out = _native.lib(), []
+    for s in range(s0, s0 + steps):
+        ms = env.get_action_mask()
+        for e, m, a in zip(env.envs, ms, acts):
+            _native.check(lib.mrts_sample_actions_src(torch.cuda.current_stream().cuda_stream, m.data_ptr(), e._src.data_ptr(),
+                                                      e.num_envs, e.height * e.width, 0, ctypes.c_uint64(9), s, a.data_ptr()))
+        o, r, d, i = env.step(acts)
+        rec = [x.clone() for x in ms] + [e._src.clone() for e in env.envs] + [x.clone() for x in o]
+        if isinstance(r, list):
+            rec += [x.clone() for x in r] + [x.clone() for x in d]
+        else:
+            rec += [r.clone(), d.clone(), torch.as_tensor(env.bucket.copy())]
+        out.append(rec)
+    return out
+
+
+def _replay_check(env, first_obs_fn, t0, t1):
+    import torch
+
+    acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=e.device) for e in env.envs]
+    _run_multi(env, 0, t0, acts)
+    at = [x.clone() for x in first_obs_fn()]
+    state = env.get_state()
+    a = _run_multi(env, t0, t1, acts)
+    back = env.set_state(state)
+    for x, y in zip(back, at):
+        assert torch.equal(x, y)
+    b = _run_multi(env, t0, t1, acts)
+    for s, (x, y) in enumerate(zip(a, b)):
+        for k, (u, v) in enumerate(zip(x, y)):
+            assert torch.equal(u, v), f"step {t0 + s} output {k}"
+    assert env.error_flags() == 0
+    return a
+
+
+def test_checkpoint_mixed_map_buckets_replays():
+    """MicroRTSMixedMapVecEnv.get_state / set_state (configs[4]'s env: 8x8 / 16x16 / 24x24
+    buckets with device bots, stepped by the grouped launch): the continuation replays bit
+    for bit."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
+
+    bk = [dict(map_paths=["maps/8x8/basesWorkers8x8.xml"], num_selfplay_envs=8, ai2s=[microrts_ai.workerRushAI] * 4),
+          dict(map_paths=["maps/16x16/basesWorkers16x16.xml"], num_selfplay_envs=8,
+               ai2s=[microrts_ai.coacAI, microrts_ai.randomBiasedAI] * 3),
+          dict(map_paths=["maps/24x24/basesWorkers24x24.xml"], num_selfplay_envs=4, ai2s=[microrts_ai.lightRushAI] * 2)]
+    env = MicroRTSMixedMapVecEnv(bk, max_steps=70, reward_weight=W, return_tensors=True, obs_dtype=torch.int32)
+    assert env.grouped
+    env.reset()
+    a = _replay_check(env, lambda: [e._obs for e in env.envs], 40, 60)
+    assert sum(int(x[-1].sum()) for x in a) > 0   # games end inside the replayed stretch
+    env.close()
+
+
+def test_checkpoint_size_cycling_replays():
+    """MicroRTSSizeCyclingVecEnv.get_state / set_state: every size engine's games, played and
+    parked, the env -> size map and the cycle position come back; the continuation (games
+    moving between sizes inside it) replays bit for bit and parked rows stay zero."""
+    import torch
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSSizeCyclingVecEnv
+
+    cyc = ["maps/8x8/basesWorkers8x8.xml", "maps/16x16/basesWorkers16x16A.xml", "maps/10x10/basesTwoWorkers10x10.xml",
+           "maps/24x24/basesWorkers24x24.xml", "maps/16x16/basesWorkers16x16C.xml"]
+    init = ["maps/16x16/basesWorkers16x16.xml"] * 4 + ["maps/8x8/basesWorkers8x8.xml"] * 2 + \
+           ["maps/10x10/basesTwoWorkers10x10.xml", "maps/16x16/basesWorkers16x16.xml", "maps/8x8/basesWorkers8x8.xml"]
+    env = MicroRTSSizeCyclingVecEnv(6, 3, ai2s=[microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.passiveAI],
+                                    map_paths=init, cycle_maps=cyc, max_steps=25, reward_weight=W, obs_dtype=torch.int32)
+    obs = env.reset()
+    moved = env.bucket.copy()
+    a = _replay_check(env, lambda: env_obs(env), 30, 70)
+    assert (np.stack([x[-1].numpy() for x in a]) != moved).any()   # envs changed size inside the replay
+    for rec in a:
+        bucket = rec[-1].numpy()
+        for i, o in enumerate(rec[2 * len(env.envs):3 * len(env.envs)]):
+            assert not o[torch.from_numpy(bucket != i).to(o.device)].any()
+    env.close()
+
+
+def env_obs(env):
+    return [e._obs for e in env.envs]
