@@ -27,6 +27,12 @@ VecMonitor (ppo_gridnet.py:384-385).  The contract is chosen by the environment
 variable alone: the env is constructed without `return_tensors`.
 
   python examples/ppo_gridnet_driver.py --num-selfplay-envs 4072 --num-bot-envs 24 --partial-obs --num-steps 8 --updates 2 --api hybrid
+
+`--eval` runs experiments/ppo_gridnet_eval.py's loop instead (`evaluate`): the reference's
+trained agent_sota.pt (committed as tests/golden/agent_sota_policy.npz) against a device bot
+(`--ai coacAI`) or against itself in selfplay:
+
+  python examples/ppo_gridnet_driver.py --eval --ai coacAI --num-steps 16 --total-timesteps 32
 """
 import argparse
 import json
@@ -288,7 +294,93 @@ def run(num_selfplay_envs=2, num_bot_envs=0, partial_obs=False, num_steps=16, up
     return stats
 
 
+def load_weights(path):
+    """A reference Agent state_dict as name -> tensor: the committed .npz fixture of
+    agent_sota.pt (tests/golden/make_agent_sota.py), or a .pt file read with
+    torch.load(weights_only=True) (never an unpickling load)."""
+    if path.endswith(".npz"):
+        with np.load(path) as z:
+            return {k: torch.from_numpy(z[k]) for k in z.files}
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+SOTA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "agent_sota_policy.npz")
+
+
+def evaluate(ai="", num_steps=256, total_timesteps=1000000, agent_model_path=SOTA, agent2_model_path=SOTA, seed=1,
+             device="cuda", log=print, render=True):
+    """experiments/ppo_gridnet_eval.py's loop over this engine: a trained GridNet (default
+    the reference's agent_sota.pt) against a device bot (`ai`, 1 bot env; :60-61) or
+    against a second trained GridNet in selfplay (2 selfplay envs, player 0 = agent and
+    player 1 = agent2 on the even / odd envs; :62-63, 170-186), basesWorkers16x16A,
+    max_steps 5000, reward_weight [10, 1, 1, 0.2, 1, 4] (:113-123), StatsRecorder +
+    VecMonitor (:124-125), render() every step (:161), the masks and steps in the
+    script's own call forms (:168, :189-190), and one WinLoss line per finished
+    episode (:195-201).  Returns the win / loss records and the step count."""
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    dev = torch.device(device)
+    ais = [getattr(microrts_ai, ai)] if ai else []
+    nbot, nsp = (1, 0) if ai else (0, 2)
+    env = MicroRTSGridModeVecEnv(num_bot_envs=nbot, num_selfplay_envs=nsp, partial_obs=False, max_steps=5000, render_theme=2,
+                                 ai2s=ais, map_paths=["maps/16x16/basesWorkers16x16A.xml"],
+                                 reward_weight=np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0]), device=dev)
+    envs = VecMonitor(StatsRecorder(env, 0.99))
+    n, hw = envs.num_envs, envs.height * envs.width
+    h, w, planes = envs.observation_space.shape
+    agent, agent2 = GridNet(planes, h, w).to(dev), GridNet(planes, h, w).to(dev)
+    assert len(agent.load_reference_state(load_weights(agent_model_path))) == 8
+    agent.eval()
+    if not ai:
+        assert len(agent2.load_reference_state(load_weights(agent2_model_path))) == 8
+        agent2.eval()
+    num_updates = total_timesteps // (n * num_steps)
+    next_obs = torch.Tensor(envs.reset()).to(dev)
+    results, global_step = [], 0
+    for _ in range(num_updates):
+        for _ in range(num_steps):
+            if render:
+                envs.render()
+            global_step += n
+            with torch.no_grad():
+                masks = torch.tensor(np.array(envs.get_action_mask())).to(dev)
+                if ai:
+                    action, _, _, _ = policy(agent, next_obs, masks, hw)
+                else:
+                    p1, _, _, _ = policy(agent, next_obs[::2], masks[::2], hw)
+                    p2, _, _, _ = policy(agent2, next_obs[1::2], masks[1::2], hw)
+                    action = torch.zeros((n,) + tuple(p2.shape[1:]), dtype=torch.long, device=dev)
+                    action[::2], action[1::2] = p1, p2
+            obs, rs, ds, infos = envs.step(action.cpu().numpy().reshape(n, -1))
+            next_obs = torch.Tensor(obs).to(dev)
+            for idx, info in enumerate(infos):
+                if "episode" in info.keys():
+                    wl = float(info["microrts_stats"]["WinLossRewardFunction"])
+                    if ai:
+                        log(f"against {ai} {wl}")
+                        results.append(("agent", wl))
+                    elif idx % 2 == 0:
+                        log(f"player{idx % 2} {wl}")
+                        results.append(("player0", wl))
+    out = {"global_step": global_step, "results": results, "engine_error_flags": env.error_flags()}
+    envs.close()
+    return out
+
+
 if __name__ == "__main__":
+    if "--eval" in sys.argv:   # ppo_gridnet_eval.py's flags
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--eval", action="store_true")
+        ap.add_argument("--ai", type=str, default="")
+        ap.add_argument("--num-steps", type=int, default=256)
+        ap.add_argument("--total-timesteps", type=int, default=1000000)
+        ap.add_argument("--agent-model-path", type=str, default=SOTA)
+        ap.add_argument("--agent2-model-path", type=str, default=SOTA)
+        ap.add_argument("--seed", type=int, default=1)
+        a = ap.parse_args()
+        out = evaluate(a.ai, a.num_steps, a.total_timesteps, a.agent_model_path, a.agent2_model_path, a.seed)
+        print(json.dumps(out))
+        sys.exit(0)
     ap = argparse.ArgumentParser()
     ap.add_argument("--num-selfplay-envs", type=int, default=2)
     ap.add_argument("--num-bot-envs", type=int, default=0)

@@ -33,3 +33,23 @@ def test_ppo_gridnet_partial_obs_with_bots(api):
     """configs[3] shape: partial_obs (31 planes) + the bot envs ppo_gridnet.py builds."""
     s = _driver().run(num_selfplay_envs=8, num_bot_envs=8, partial_obs=True, num_steps=8, updates=2, api=api, log=lambda _: None)
     assert s["global_step"] == 2 * 8 * 16 and s["finite"] and s["engine_error_flags"] == 0
+
+
+def test_ppo_gridnet_eval_selfplay():
+    """test_e2e.py:17-26: ppo_gridnet_eval.py --num-steps 16 --total-timesteps 32 (2 selfplay
+    envs, the reference's agent_sota.pt on both sides, render() every step)."""
+    out = _driver().evaluate(num_steps=16, total_timesteps=32, log=lambda _: None)
+    assert out["global_step"] == 32 and out["engine_error_flags"] == 0
+
+
+def test_ppo_gridnet_eval_bot():
+    """test_e2e.py:29-35: ppo_gridnet_eval.py --ai coacAI --num-steps 16 --total-timesteps 32;
+    and a longer run in which agent_sota.pt finishes games against the device coacAI."""
+    d = _driver()
+    out = d.evaluate(ai="coacAI", num_steps=16, total_timesteps=32, log=lambda _: None)
+    assert out["global_step"] == 32 and out["engine_error_flags"] == 0
+    lines = []
+    out = d.evaluate(ai="coacAI", num_steps=500, total_timesteps=3000, log=lines.append, render=False)
+    assert out["engine_error_flags"] == 0 and out["results"], "no episode ended in 3000 steps"
+    assert all(x.startswith("against coacAI ") for x in lines)
+    assert all(r in (-1.0, 0.0, 1.0) for _, r in out["results"])
