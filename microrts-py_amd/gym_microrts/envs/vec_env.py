@@ -582,15 +582,21 @@ class MicroRTSGridModeVecEnv:
         _native.check(_native.lib().mrts_save_state(self._h, self._stream(), state.data_ptr()), self._h, "save_state")
         return EnvState(state, list(self._game_map), self.next_map.drawn)
 
-    def set_state(self, state):
-        """Restore a get_state() snapshot of this env (mrts_load_state) and return the
-        restored state's obs, as reset() does; the next get_action_mask() / step()
-        continue from it bit for bit as the saved run did (map cycling included)."""
+    def _check_state(self, state):
+        """The snapshot tensor of a get_state() EnvState that fits this env, or ValueError
+        (the engine's own fingerprint check runs in mrts_load_state)."""
         t = state.tensor if isinstance(state, EnvState) else None
         if t is None or t.device != self.device or t.dtype != torch.uint8 or t.data_ptr() % 256:
             raise ValueError("set_state expects an EnvState returned by get_state() of this env")
         if t.numel() != int(_native.lib().mrts_state_bytes(self._h)) or not t.is_contiguous():
             raise ValueError("set_state: the snapshot's size differs from this env's (another configuration)")
+        return t
+
+    def set_state(self, state):
+        """Restore a get_state() snapshot of this env (mrts_load_state) and return the
+        restored state's obs, as reset() does; the next get_action_mask() / step()
+        continue from it bit for bit as the saved run did (map cycling included)."""
+        t = self._check_state(state)
         self._mask_prefetch = None
         _native.check(_native.lib().mrts_load_state(self._h, self._stream(), t.data_ptr(), self._obs.data_ptr()), self._h,
                       "load_state")
@@ -935,6 +941,8 @@ class MicroRTSMixedMapVecEnv:
         """Restore a get_state() list of this env; returns the restored obs per bucket."""
         if len(states) != len(self.envs):
             raise ValueError(f"set_state expects {len(self.envs)} bucket states, got {len(states)}")
+        for e, st in zip(self.envs, states):   # every bucket checked before any is overwritten
+            e._check_state(st)
         return [e.set_state(st) for e, st in zip(self.envs, states)]
 
     def close(self):
@@ -1072,8 +1080,11 @@ class MicroRTSSizeCyclingVecEnv:
 
     def set_state(self, state):
         """Restore a get_state() snapshot of this env; returns the restored obs per size."""
-        if not isinstance(state, SizeCyclingState) or len(state.engines) != len(self.envs):
+        if not isinstance(state, SizeCyclingState) or len(state.engines) != len(self.envs) or \
+                len(state.bucket) != self.num_envs:
             raise ValueError("set_state expects a SizeCyclingState returned by get_state() of this env")
+        for e, st in zip(self.envs, state.engines):   # every engine checked before any is overwritten
+            e._check_state(st)
         out = [e.set_state(st) for e, st in zip(self.envs, state.engines)]
         self.bucket = state.bucket.copy()
         self.next_map = MapCycle(self.cycle_maps, state.drawn)

@@ -250,3 +250,30 @@ def test_checkpoint_size_cycling_replays():
 
 def env_obs(env):
     return [e._obs for e in env.envs]
+
+
+def test_checkpoint_mixed_map_refuses_before_overwriting():
+    """A bucket list in the wrong order (or of the wrong length) is refused before any bucket
+    is overwritten: the env keeps stepping as if set_state had not been called."""
+    import torch
+
+    from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
+
+    bk = [dict(map_paths=["maps/8x8/basesWorkers8x8.xml"], num_selfplay_envs=4),
+          dict(map_paths=["maps/16x16/basesWorkers16x16.xml"], num_selfplay_envs=4)]
+    env = MicroRTSMixedMapVecEnv(bk, max_steps=70, reward_weight=W, return_tensors=True, obs_dtype=torch.int32)
+    env.reset()
+    acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=e.device) for e in env.envs]
+    _run_multi(env, 0, 10, acts)
+    st = env.get_state()
+    a = _run_multi(env, 10, 5, acts)
+    env.set_state(st)
+    with pytest.raises(ValueError):
+        env.set_state(st[::-1])
+    with pytest.raises(ValueError):
+        env.set_state(st[:1])
+    b = _run_multi(env, 10, 5, acts)
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    env.close()
