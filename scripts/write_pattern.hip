@@ -19,6 +19,15 @@
 //   mode 13 as 8 (256 workgroups) with non-temporal stores
 //   mode 14 games' runs (phase B order) by 256 persistent workgroups (game b, b + 256, ...)
 //   mode 15 games' runs by 1024 persistent workgroups, mode 16 by 512
+//   mode 17 as 0 with each game's runs started at a rotated 4 KB chunk (g mod 8), wrapping round
+//   mode 18 as 0 with the obs and mask runs interleaved chunk by chunk
+//   mode 19 as 0 with 32 contiguous bytes per lane (two adjacent 16-B stores, 8 KB per iteration)
+//   mode 20 as 0 with each run written back to front
+//   mode 21 as 0 with every workgroup writing the mask run first, then the obs run
+//   mode 22 as 0 with a permuted game order (odd games g and g ^ 2 swapped)
+//   mode 23 games' runs by 256 persistent workgroups, each a contiguous block of G / 256 games
+//   mode 24 as 23 on 512 workgroups, mode 25 on 1024, mode 26 on 128
+//   mode 27 block fill: each of 256 workgroups writes its contiguous 1/256 of each buffer
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/write_pattern scripts/write_pattern.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -44,6 +53,23 @@ __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, 
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     if (mode >= 8 && mode <= 10) mode = 3;
     if (mode == 13) mode = 5;
+    if (mode >= 23 && mode <= 26) {   // block-distributed games: workgroup b writes games [b * G / n, (b + 1) * G / n)
+        const int no = NV * HW * P / 4, nm = NV * HW * CH / 4, per = G / gridDim.x;
+        for (int g = blockIdx.x * per; g < (blockIdx.x + 1) * per; g++) {
+            int* o = obs + (size_t)g * NV * HW * P;
+            int* m = mask + (size_t)g * NV * HW * CH;
+            for (int k = t; k < no; k += 256) st(o + 4 * k, k, salt);
+            for (int k = t; k < nm; k += 256) st(m + 4 * k, k, salt);
+        }
+        return;
+    }
+    if (mode == 27) {
+        const long long nobs = (long long)G * NV * HW * P / 4, nmask = (long long)G * NV * HW * CH / 4;
+        const long long po = nobs / gridDim.x, pm = nmask / gridDim.x;
+        for (long long k = blockIdx.x * po + t; k < (blockIdx.x + 1) * po; k += 256) st(obs + 4 * k, (int)k, salt);
+        for (long long k = blockIdx.x * pm + t; k < (blockIdx.x + 1) * pm; k += 256) st(mask + 4 * k, (int)k, salt);
+        return;
+    }
     if (mode >= 14 && mode <= 16) {
         const int no = NV * HW * P / 4, nm = NV * HW * CH / 4;
         for (int g = blockIdx.x; g < G; g += gridDim.x) {
@@ -64,12 +90,39 @@ __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, 
         return;
     }
     const int g = blockIdx.x;
+    if (mode == 22) {   // swizzle: which game a workgroup writes (a permutation of 0..G-1)
+        const int gg = (g & 1) ? (g ^ 2) : g;
+        int* o = obs + (size_t)gg * NV * HW * P;
+        int* m = mask + (size_t)gg * NV * HW * CH;
+        const int no = NV * HW * P / 4, nm = NV * HW * CH / 4;
+        for (int k = t; k < no; k += 256) st(o + 4 * k, k, salt);
+        for (int k = t; k < nm; k += 256) st(m + 4 * k, k, salt);
+        return;
+    }
     int* o = obs + (size_t)g * NV * HW * P;
     int* m = mask + (size_t)g * NV * HW * CH;
     const int no = NV * HW * P / 4, nm = NV * HW * CH / 4;   // 16-B stores per game
     if (mode == 0) {
         for (int k = t; k < no; k += 256) st(o + 4 * k, k, salt);
         for (int k = t; k < nm; k += 256) st(m + 4 * k, k, salt);
+    } else if (mode == 17) {
+        const int rot = (g & 7) * 256;   // in 16-B stores: 4 KB chunks
+        for (int k = t; k < no; k += 256) { const int j = (k + rot) % no; st(o + 4 * j, j, salt); }
+        for (int k = t; k < nm; k += 256) { const int j = (k + rot) % nm; st(m + 4 * j, j, salt); }
+    } else if (mode == 18) {
+        for (int k = t; k < nm; k += 256) {
+            if (k < no) st(o + 4 * k, k, salt);
+            st(m + 4 * k, k, salt);
+        }
+    } else if (mode == 19) {
+        for (int k = 2 * t; k < no; k += 512) { st(o + 4 * k, k, salt); if (k + 1 < no) st(o + 4 * k + 4, k + 1, salt); }
+        for (int k = 2 * t; k < nm; k += 512) { st(m + 4 * k, k, salt); if (k + 1 < nm) st(m + 4 * k + 4, k + 1, salt); }
+    } else if (mode == 20) {
+        for (int k = t; k < no; k += 256) { const int j = no - 1 - k; st(o + 4 * j, j, salt); }
+        for (int k = t; k < nm; k += 256) { const int j = nm - 1 - k; st(m + 4 * j, j, salt); }
+    } else if (mode == 21) {
+        for (int k = t; k < nm; k += 256) st(m + 4 * k, k, salt);
+        for (int k = t; k < no; k += 256) st(o + 4 * k, k, salt);
     } else if (mode == 11 || mode == 12) {
         const int nt = mode == 11 ? 128 : 64;
         if (t >= nt) return;
@@ -101,10 +154,13 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[17] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
+    const char* names[28] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
                              "grid_stride_constant", "grid_stride_nontemporal", "phaseB_constant", "hipMemsetD32",
                              "grid_stride_256wg", "grid_stride_512wg", "grid_stride_1024wg", "phaseB_2waves", "phaseB_1wave",
-                             "grid_stride_256wg_nt", "games_256_persistent", "games_1024_persistent", "games_512_persistent"};
+                             "grid_stride_256wg_nt", "games_256_persistent", "games_1024_persistent", "games_512_persistent",
+                             "phaseB_rotated_start", "phaseB_obs_mask_interleaved", "phaseB_32B_per_lane", "phaseB_back_to_front",
+                             "phaseB_mask_first", "phaseB_game_swizzle", "games_256_block", "games_512_block",
+                             "games_1024_block", "games_128_block", "block_fill_256wg"};
     auto launch = [&](int mode, int grid, int i) {
         if (mode == 7) {
             hipMemsetD32Async((hipDeviceptr_t)obs, i, bo / 4, 0);
@@ -114,9 +170,10 @@ int main() {
         }
     };
     for (int round = 0; round < 3; round++) {
-        for (int mode = 0; mode < 17; mode++) {
-            const int grid = (mode >= 3 && mode <= 5) ? 256 * 7 : (mode == 8 || mode == 13 || mode == 14) ? 256
-                           : (mode == 9 || mode == 16) ? 512 : (mode == 10 || mode == 15) ? 1024 : G;
+        for (int mode = 0; mode < 28; mode++) {
+            const int grid = (mode >= 3 && mode <= 5) ? 256 * 7 : (mode == 8 || mode == 13 || mode == 14 || mode == 23 || mode == 27) ? 256
+                           : (mode == 9 || mode == 16 || mode == 24) ? 512 : (mode == 10 || mode == 15 || mode == 25) ? 1024
+                           : mode == 26 ? 128 : G;
             for (int i = 0; i < 5; i++) launch(mode, grid, i);
             hipEventRecord(a);
             const int it = 50;
