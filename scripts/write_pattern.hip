@@ -28,6 +28,10 @@
 //   mode 23 games' runs by 256 persistent workgroups, each a contiguous block of G / 256 games
 //   mode 24 as 23 on 512 workgroups, mode 25 on 1024, mode 26 on 128
 //   mode 27 block fill: each of 256 workgroups writes its contiguous 1/256 of each buffer
+//   mode 28 emit proxy: as 8 (grid-stride, 256 workgroups), every 16-B store's words built from
+//           the game state (int4 per cell, 4 KB per game): obs stores read their cell(s), mask
+//           stores their cell and its 4 neighbours -- the emit kernel of a logic / emit split
+//   mode 29 as 28 on 512 workgroups, mode 30 on 1792
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/write_pattern scripts/write_pattern.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -47,6 +51,45 @@ __device__ __forceinline__ void stc(int* p, int salt) {
 __device__ __forceinline__ void stnt(int* p, int k, int salt) {
     v4i v = {k ^ salt, k + 1, k + 2, salt};
     __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(p));
+}
+
+__device__ __forceinline__ int cellword(const int4* __restrict__ state, int g, int c) {
+    const int4 u = state[(size_t)g * HW + c];
+    return (u.x & 15) | ((u.x >> 4 & 3) << 4) | ((u.z & 7) << 8) | (u.w & 0xff) << 12;
+}
+
+__global__ __launch_bounds__(256) void k_emit_proxy(int* obs, int* mask, const int4* __restrict__ state, int G, int salt) {
+    const int t = threadIdx.x;
+    const long long nobs = (long long)G * NV * HW * P / 4, nmask = (long long)G * NV * HW * CH / 4;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long k = blockIdx.x * 256ll + t; k < nobs; k += stride) {
+        const long long f0 = 4 * k;                       // first float of the store
+        const long long e = f0 / (HW * P);                // env
+        const int r = (int)(f0 - e * HW * P), c = r / P, ch = r - c * P;
+        const int g = (int)(e >> 1);
+        const int a = cellword(state, g, c);
+        const int b = ch + 3 >= P && c + 1 < HW ? cellword(state, g, c + 1) : a;
+        v4i v;
+        for (int q = 0; q < 4; q++) {
+            const int chq = ch + q, src = chq >= P ? b : a, cc = chq >= P ? chq - P : chq;
+            v[q] = __float_as_int(((src >> (cc & 15)) & 1) ? 1.0f : 0.0f);
+        }
+        *reinterpret_cast<v4i*>(obs + 4 * k) = v;
+    }
+    for (long long k = blockIdx.x * 256ll + t; k < nmask; k += stride) {
+        const long long i0 = 4 * k;
+        const long long e = i0 / (HW * CH);
+        const int r = (int)(i0 - e * HW * CH), c = r / CH, ch = r - c * CH;
+        const int g = (int)(e >> 1), x = c % 16, y = c / 16;
+        int acc = cellword(state, g, c);
+        if (y > 0) acc ^= cellword(state, g, c - 16) << 1;
+        if (x < 15) acc ^= cellword(state, g, c + 1) << 2;
+        if (y < 15) acc ^= cellword(state, g, c + 16) << 3;
+        if (x > 0) acc ^= cellword(state, g, c - 1) << 4;
+        v4i v;
+        for (int q = 0; q < 4; q++) v[q] = (acc >> ((ch + q) & 31)) & 1;
+        *reinterpret_cast<v4i*>(mask + 4 * k) = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, int G, int salt) {
@@ -151,18 +194,25 @@ int main() {
     const size_t bo = (size_t)G * NV * HW * P * 4, bm = (size_t)G * NV * HW * CH * 4;
     hipMalloc(&obs, bo);
     hipMalloc(&mask, bm);
+    int* state;   // 4 KB of int4 cells per game, arbitrary contents
+    hipMalloc(&state, (size_t)G * HW * 16);
+    hipMemset(state, 0x5a, (size_t)G * HW * 16);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[28] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
+    const char* names[31] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
                              "grid_stride_constant", "grid_stride_nontemporal", "phaseB_constant", "hipMemsetD32",
                              "grid_stride_256wg", "grid_stride_512wg", "grid_stride_1024wg", "phaseB_2waves", "phaseB_1wave",
                              "grid_stride_256wg_nt", "games_256_persistent", "games_1024_persistent", "games_512_persistent",
                              "phaseB_rotated_start", "phaseB_obs_mask_interleaved", "phaseB_32B_per_lane", "phaseB_back_to_front",
                              "phaseB_mask_first", "phaseB_game_swizzle", "games_256_block", "games_512_block",
-                             "games_1024_block", "games_128_block", "block_fill_256wg"};
+                             "games_1024_block", "games_128_block", "block_fill_256wg", "emit_proxy_256wg",
+                             "emit_proxy_512wg", "emit_proxy_1792wg"};
     auto launch = [&](int mode, int grid, int i) {
-        if (mode == 7) {
+        if (mode >= 28) {
+            hipLaunchKernelGGL(k_emit_proxy, dim3(mode == 28 ? 256 : mode == 29 ? 512 : 1792), dim3(256), 0, 0, obs, mask,
+                               (const int4*)state, G, i);
+        } else if (mode == 7) {
             hipMemsetD32Async((hipDeviceptr_t)obs, i, bo / 4, 0);
             hipMemsetD32Async((hipDeviceptr_t)mask, i, bm / 4, 0);
         } else {
@@ -170,7 +220,7 @@ int main() {
         }
     };
     for (int round = 0; round < 3; round++) {
-        for (int mode = 0; mode < 28; mode++) {
+        for (int mode = 0; mode < 31; mode++) {
             const int grid = (mode >= 3 && mode <= 5) ? 256 * 7 : (mode == 8 || mode == 13 || mode == 14 || mode == 23 || mode == 27) ? 256
                            : (mode == 9 || mode == 16 || mode == 24) ? 512 : (mode == 10 || mode == 15 || mode == 25) ? 1024
                            : mode == 26 ? 128 : G;
