@@ -694,6 +694,24 @@ class MapCycle:
         return m
 
 
+def _set_states_atomic(envs, states):
+    """set_state on several engines as one operation: every snapshot is checked first, and if
+    an engine still refuses its snapshot (mrts_load_state's configuration fingerprint), the
+    engines restored before it are rolled back to where they were."""
+    for e, st in zip(envs, states):
+        e._check_state(st)
+    before = [e.get_state() for e in envs]
+    out = []
+    try:
+        for e, st in zip(envs, states):
+            out.append(e.set_state(st))
+    except Exception:
+        for e, st in zip(envs[:len(out)], before):
+            e.set_state(st)
+        raise
+    return out
+
+
 class EnvState:
     """An env-state checkpoint (MicroRTSGridModeVecEnv.get_state): the engine's
     snapshot (a 256-byte aligned device uint8 tensor, mrts_save_state) and the
@@ -941,9 +959,7 @@ class MicroRTSMixedMapVecEnv:
         """Restore a get_state() list of this env; returns the restored obs per bucket."""
         if len(states) != len(self.envs):
             raise ValueError(f"set_state expects {len(self.envs)} bucket states, got {len(states)}")
-        for e, st in zip(self.envs, states):   # every bucket checked before any is overwritten
-            e._check_state(st)
-        return [e.set_state(st) for e, st in zip(self.envs, states)]
+        return _set_states_atomic(self.envs, states)
 
     def close(self):
         for e in self.envs:
@@ -1083,9 +1099,7 @@ class MicroRTSSizeCyclingVecEnv:
         if not isinstance(state, SizeCyclingState) or len(state.engines) != len(self.envs) or \
                 len(state.bucket) != self.num_envs:
             raise ValueError("set_state expects a SizeCyclingState returned by get_state() of this env")
-        for e, st in zip(self.envs, state.engines):   # every engine checked before any is overwritten
-            e._check_state(st)
-        out = [e.set_state(st) for e, st in zip(self.envs, state.engines)]
+        out = _set_states_atomic(self.envs, state.engines)
         self.bucket = state.bucket.copy()
         self.next_map = MapCycle(self.cycle_maps, state.drawn)
         return out

@@ -277,3 +277,40 @@ def test_checkpoint_mixed_map_refuses_before_overwriting():
         for u, v in zip(x, y):
             assert torch.equal(u, v)
     env.close()
+
+
+def test_checkpoint_mixed_map_rolls_back_on_refusal():
+    """Snapshots of a same-shape mixed env whose second bucket plays other bots: the first
+    bucket's snapshot fits and loads, the second is refused by the engine's configuration
+    fingerprint, and the first bucket is rolled back -- the env continues as if set_state had
+    not been called."""
+    import torch
+
+    from gym_microrts import _native, microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
+
+    def make(bot):
+        bk = [dict(map_paths=["maps/8x8/basesWorkers8x8.xml"], num_selfplay_envs=4),
+              dict(map_paths=["maps/16x16/basesWorkers16x16.xml"], num_selfplay_envs=2, ai2s=[bot] * 2)]
+        return MicroRTSMixedMapVecEnv(bk, max_steps=70, reward_weight=W, return_tensors=True, obs_dtype=torch.int32)
+
+    env, other = make(microrts_ai.workerRushAI), make(microrts_ai.lightRushAI)
+    for e in (env, other):
+        e.reset()
+    for e, o in zip(env.envs, other.envs):   # same shapes: only the engine's fingerprint tells them apart
+        assert int(_native.lib().mrts_state_bytes(e._h)) == int(_native.lib().mrts_state_bytes(o._h))
+    acts = [torch.empty((e.num_envs, e.height * e.width, 7), dtype=torch.int64, device=e.device) for e in env.envs]
+    _run_multi(other, 0, 7, acts)
+    foreign = other.get_state()
+    _run_multi(env, 0, 10, acts)
+    st = env.get_state()
+    a = _run_multi(env, 10, 5, acts)
+    env.set_state(st)
+    with pytest.raises(_native.MicroRTSError):
+        env.set_state(foreign)
+    b = _run_multi(env, 10, 5, acts)
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    env.close()
+    other.close()
