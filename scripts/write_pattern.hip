@@ -32,6 +32,11 @@
 //           the game state (int4 per cell, 4 KB per game): obs stores read their cell(s), mask
 //           stores their cell and its 4 neighbours -- the emit kernel of a logic / emit split
 //   mode 29 as 28 on 512 workgroups, mode 30 on 1792
+//   mode 31 pipelined emit proxy (timing only): 256 workgroups walk the grid-stride window of 4 KB
+//           chunks; each step's game state (4 KB, one int4 per lane) is loaded D = 8 steps ahead
+//           into registers, parked in LDS when its step comes, and the chunk's words are built from
+//           LDS (cell + 4 neighbours) -- what a logic / emit split's emit kernel would have to do
+//   mode 32 as 31 with D = 16, mode 33 as 31 on 512 workgroups
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/write_pattern scripts/write_pattern.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -58,38 +63,73 @@ __device__ __forceinline__ int cellword(const int4* __restrict__ state, int g, i
     return (u.x & 15) | ((u.x >> 4 & 3) << 4) | ((u.z & 7) << 8) | (u.w & 0xff) << 12;
 }
 
-__global__ __launch_bounds__(256) void k_emit_proxy(int* obs, int* mask, const int4* __restrict__ state, int G, int salt) {
-    const int t = threadIdx.x;
-    const long long nobs = (long long)G * NV * HW * P / 4, nmask = (long long)G * NV * HW * CH / 4;
-    const long long stride = (long long)gridDim.x * 256;
-    for (long long k = blockIdx.x * 256ll + t; k < nobs; k += stride) {
-        const long long f0 = 4 * k;                       // first float of the store
-        const long long e = f0 / (HW * P);                // env
-        const int r = (int)(f0 - e * HW * P), c = r / P, ch = r - c * P;
-        const int g = (int)(e >> 1);
-        const int a = cellword(state, g, c);
-        const int b = ch + 3 >= P && c + 1 < HW ? cellword(state, g, c + 1) : a;
-        v4i v;
-        for (int q = 0; q < 4; q++) {
-            const int chq = ch + q, src = chq >= P ? b : a, cc = chq >= P ? chq - P : chq;
-            v[q] = __float_as_int(((src >> (cc & 15)) & 1) ? 1.0f : 0.0f);
-        }
-        *reinterpret_cast<v4i*>(obs + 4 * k) = v;
-    }
-    for (long long k = blockIdx.x * 256ll + t; k < nmask; k += stride) {
-        const long long i0 = 4 * k;
-        const long long e = i0 / (HW * CH);
-        const int r = (int)(i0 - e * HW * CH), c = r / CH, ch = r - c * CH;
-        const int g = (int)(e >> 1), x = c % 16, y = c / 16;
+// one buffer of the proxy: store k (16 B) of game g's run; constant divisors, 32-bit math
+template <int WIDTH, bool NB>
+__device__ __forceinline__ void emit_direct(int* out, const int4* __restrict__ state, int G, int salt) {
+    constexpr int PER = NV * HW * WIDTH / 4;   // 16-B stores per game
+    const unsigned n = (unsigned)G * PER, stride = gridDim.x * 256u;
+    for (unsigned k = blockIdx.x * 256u + threadIdx.x; k < n; k += stride) {
+        const unsigned g = k / PER, w0 = 4 * (k - g * PER), c2 = w0 / WIDTH, ch = w0 - c2 * WIDTH, c = c2 & (HW - 1);
+        const int x = c & 15, y = c >> 4;
         int acc = cellword(state, g, c);
-        if (y > 0) acc ^= cellword(state, g, c - 16) << 1;
-        if (x < 15) acc ^= cellword(state, g, c + 1) << 2;
-        if (y < 15) acc ^= cellword(state, g, c + 16) << 3;
-        if (x > 0) acc ^= cellword(state, g, c - 1) << 4;
+        if (NB) {
+            if (y > 0) acc ^= cellword(state, g, c - 16) << 1;
+            if (x < 15) acc ^= cellword(state, g, c + 1) << 2;
+            if (y < 15) acc ^= cellword(state, g, c + 16) << 3;
+            if (x > 0) acc ^= cellword(state, g, c - 1) << 4;
+        } else if (ch + 3 >= WIDTH && c + 1 < HW) {
+            acc ^= cellword(state, g, c + 1) << 5;
+        }
         v4i v;
-        for (int q = 0; q < 4; q++) v[q] = (acc >> ((ch + q) & 31)) & 1;
-        *reinterpret_cast<v4i*>(mask + 4 * k) = v;
+        for (int q = 0; q < 4; q++) v[q] = ((acc >> ((ch + q) & 31)) & 1) ^ salt;
+        *reinterpret_cast<v4i*>(out + 4 * (size_t)k) = v;
     }
+}
+
+__global__ __launch_bounds__(256) void k_emit_proxy(int* obs, int* mask, const int4* __restrict__ state, int G, int salt) {
+    emit_direct<P, false>(obs, state, G, salt);
+    emit_direct<CH, true>(mask, state, G, salt);
+}
+
+template <int D, int WIDTH, bool NB>
+__device__ __forceinline__ void emit_pipe(int* out, const int4* __restrict__ state, int G, int salt, int* lw) {
+    constexpr int PER = NV * HW * WIDTH / 4;
+    const int t = threadIdx.x;
+    const unsigned n = (unsigned)G * PER, stride = gridDim.x * 256u, first = blockIdx.x * 256u;
+    int4 ring[D];
+#pragma unroll
+    for (int d = 0; d < D; d++) ring[d] = state[(size_t)min((unsigned)G - 1, (first + d * stride) / PER) * HW + t];
+    for (unsigned k0 = first; k0 < n; k0 += stride) {
+        const int4 u = ring[0];
+#pragma unroll
+        for (int d = 0; d + 1 < D; d++) ring[d] = ring[d + 1];
+        ring[D - 1] = state[(size_t)min((unsigned)G - 1, (k0 + D * stride) / PER) * HW + t];
+        __syncthreads();
+        lw[t] = (u.x & 15) | ((u.x >> 4 & 3) << 4) | ((u.z & 7) << 8) | (u.w & 0xff) << 12;
+        __syncthreads();
+        const unsigned k = k0 + t;
+        if (k < n) {
+            const unsigned g0 = k0 / PER, w0 = 4 * (k - g0 * PER), c2 = w0 / WIDTH, ch = w0 - c2 * WIDTH, c = c2 & (HW - 1);
+            const int x = c & 15, y = c >> 4;
+            int acc = lw[c];
+            if (NB) {
+                if (y > 0) acc ^= lw[c - 16] << 1;
+                if (x < 15) acc ^= lw[c + 1] << 2;
+                if (y < 15) acc ^= lw[c + 16] << 3;
+                if (x > 0) acc ^= lw[c - 1] << 4;
+            }
+            v4i v;
+            for (int q = 0; q < 4; q++) v[q] = ((acc >> ((ch + q) & 31)) & 1) ^ salt;
+            *reinterpret_cast<v4i*>(out + 4 * (size_t)k) = v;
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_emit_pipe(int* obs, int* mask, const int4* __restrict__ state, int G, int salt) {
+    __shared__ int lw[HW];   // the step's game, one word per cell
+    emit_pipe<D, P, false>(obs, state, G, salt, lw);
+    emit_pipe<D, CH, true>(mask, state, G, salt, lw);
 }
 
 __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, int G, int salt) {
@@ -200,16 +240,22 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[31] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
+    const char* names[34] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
                              "grid_stride_constant", "grid_stride_nontemporal", "phaseB_constant", "hipMemsetD32",
                              "grid_stride_256wg", "grid_stride_512wg", "grid_stride_1024wg", "phaseB_2waves", "phaseB_1wave",
                              "grid_stride_256wg_nt", "games_256_persistent", "games_1024_persistent", "games_512_persistent",
                              "phaseB_rotated_start", "phaseB_obs_mask_interleaved", "phaseB_32B_per_lane", "phaseB_back_to_front",
                              "phaseB_mask_first", "phaseB_game_swizzle", "games_256_block", "games_512_block",
                              "games_1024_block", "games_128_block", "block_fill_256wg", "emit_proxy_256wg",
-                             "emit_proxy_512wg", "emit_proxy_1792wg"};
+                             "emit_proxy_512wg", "emit_proxy_1792wg", "emit_pipe_D8_256wg",
+                             "emit_pipe_D16_256wg", "emit_pipe_D8_512wg"};
     auto launch = [&](int mode, int grid, int i) {
-        if (mode >= 28) {
+        if (mode >= 31) {
+            if (mode == 32)
+                hipLaunchKernelGGL(k_emit_pipe<16>, dim3(256), dim3(256), 0, 0, obs, mask, (const int4*)state, G, i);
+            else
+                hipLaunchKernelGGL(k_emit_pipe<8>, dim3(mode == 33 ? 512 : 256), dim3(256), 0, 0, obs, mask, (const int4*)state, G, i);
+        } else if (mode >= 28) {
             hipLaunchKernelGGL(k_emit_proxy, dim3(mode == 28 ? 256 : mode == 29 ? 512 : 1792), dim3(256), 0, 0, obs, mask,
                                (const int4*)state, G, i);
         } else if (mode == 7) {
@@ -220,7 +266,7 @@ int main() {
         }
     };
     for (int round = 0; round < 3; round++) {
-        for (int mode = 0; mode < 31; mode++) {
+        for (int mode = 0; mode < 34; mode++) {
             const int grid = (mode >= 3 && mode <= 5) ? 256 * 7 : (mode == 8 || mode == 13 || mode == 14 || mode == 23 || mode == 27) ? 256
                            : (mode == 9 || mode == 16 || mode == 24) ? 512 : (mode == 10 || mode == 15 || mode == 25) ? 1024
                            : mode == 26 ? 128 : G;
