@@ -85,6 +85,9 @@ def parse(argv=None):
                     help="mixed workload: the buckets' steps in one mrts_step_group call with this policy "
                          "(MRTS_GROUP_* bits, include/microrts_amd.h; default = merge-fit | bots-first), "
                          "or 'none' = one step launch per bucket")
+    ap.add_argument("--sampler-group", type=int, default=1, choices=[0, 1],
+                    help="mixed workload, src sampler: 1 = every bucket's actions in one "
+                         "mrts_sample_actions_src_group launch, 0 = one launch per bucket (same actions)")
     ap.add_argument("--dump", default=None,
                     help="save each rank's final obs / masks / raw rewards / dones to DUMP.rank<r>.npz (shard tests)")
     return ap.parse_args(argv)
@@ -193,13 +196,25 @@ def run_mixed(args, rank, world, dev):
     ev = {}
     timing = [False]
 
+    # the stand-in policy over every bucket in one launch (mrts_sample_actions_src_group:
+    # each bucket's actions are those of its own mrts_sample_actions_src call)
+    grouped_sampler = bool(args.sampler_group) and args.sampler == "src" and len(env.envs) <= _native.SAMPLE_GROUP_MAX
+
     def one_step(s):
         masks = env.get_action_mask()
         rec = timing[0]
-        for e, m, a in zip(env.envs, masks, acts):
+        for e in env.envs:
             e.kernel_events = ev.setdefault(e.height, {}) if rec else None
-            _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, rank * e.num_envs,
-                                 seed, s, a), None, "sample")
+        if grouped_sampler:
+            segs = (_native.SampleSeg * len(env.envs))(*[
+                _native.SampleSeg(m.data_ptr(), e.source_unit_mask.data_ptr(), e.num_envs, e.height * e.width, rank * e.num_envs,
+                                  a.data_ptr()) for e, m, a in zip(env.envs, masks, acts)])
+            _native.check(lib.mrts_sample_actions_src_group(torch.cuda.current_stream().cuda_stream, segs, len(env.envs), seed, s),
+                          None, "sample_group")
+        else:
+            for e, m, a in zip(env.envs, masks, acts):
+                _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, rank * e.num_envs,
+                                     seed, s, a), None, "sample")
         if not rec:
             return env.step(acts)
         # the buckets' step kernels run concurrently: time them together too
@@ -242,6 +257,7 @@ def run_mixed(args, rank, world, dev):
     stats["buckets_concurrent"] = env.concurrent
     stats["group_policy"] = env.group_policy if env.grouped else None
     stats["bucket_launch"], stats["launches_per_step"] = env.launch_plan()
+    stats["sampler_launches_per_step"] = 1 if grouped_sampler else len(env.envs)
     if ev.get("all"):
         stats["step_all_buckets_ms"] = float(np.mean([a.elapsed_time(b) for a, b in ev["all"]]))
     return elapsed, {}, env.error_flags(), 256, sum(e._n_games() for e in env.envs), env.num_envs, 29, 0, stats

@@ -223,6 +223,20 @@ int mrts_sample_actions(void *stream, const int32_t *mask, int32_t num_envs, int
 int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *source, int32_t num_envs, int32_t hw,
                             int32_t env0, uint64_t seed, uint32_t step, int64_t *actions);
 
+/* mrts_sample_actions_src over up to MRTS_SAMPLE_GROUP_MAX batches at once (the map-size
+ * buckets of one mixed batch) in ONE launch: segment k's actions are exactly those
+ * mrts_sample_actions_src(stream, seg.mask, seg.source, seg.num_envs, seg.hw, seg.env0,
+ * seed, step, seg.actions) writes.  Each segment: num_envs * hw below 2^31 - 256,
+ * actions 16-byte aligned; MRTS_EINVAL otherwise.  The bench's stand-in policy. */
+#define MRTS_SAMPLE_GROUP_MAX 4
+typedef struct mrts_sample_seg {
+    const int32_t *mask;     /* [num_envs][hw][78] */
+    const int32_t *source;   /* [num_envs][hw] */
+    int32_t num_envs, hw, env0;
+    int64_t *actions;        /* [num_envs][hw][7] */
+} mrts_sample_seg;
+int mrts_sample_actions_src_group(void *stream, const mrts_sample_seg *segs, int32_t nseg, uint64_t seed, uint32_t step);
+
 /* Per-game rollout statistics, host int32 out[num_games][MRTS_GAME_STATS]:
  * game time (ticks since the game's last reset; the reference's gs.getTime()),
  * env steps of the episode, steps since creation, and three never-reset

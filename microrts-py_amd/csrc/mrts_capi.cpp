@@ -707,6 +707,17 @@ int mrts_sample_actions_src(void *stream, const int32_t *mask, const int32_t *so
     return mrts_engine_sample_src(mask, source, n, hw, env0, seed, step, actions, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
 }
 
+int mrts_sample_actions_src_group(void *stream, const mrts_sample_seg *segs, int32_t nseg, uint64_t seed, uint32_t step) {
+    if (!segs || nseg < 1 || nseg > MRTS_SAMPLE_GROUP_MAX) return MRTS_EINVAL;
+    for (int k = 0; k < nseg; k++) {
+        const mrts_sample_seg &q = segs[k];
+        if (!q.mask || !q.source || !q.actions || q.num_envs < 0 || q.hw <= 0 || q.env0 < 0) return MRTS_EINVAL;
+        if ((int64_t)q.num_envs * q.hw > (int64_t)INT32_MAX - 256) return MRTS_EINVAL;   // 32-bit row indexing
+        if ((uintptr_t)q.actions & 15u) return MRTS_EINVAL;   // the rows' 16-byte stores
+    }
+    return mrts_engine_sample_src_group(segs, nseg, seed, step, (hipStream_t)stream) ? MRTS_EHIP : MRTS_OK;
+}
+
 int mrts_bind_mask_outputs(mrts_vec *h, int32_t *mask, int32_t *source) {
     if (!bound(h)) return fail(h, MRTS_ESTATE, "bind_mask_outputs: workspace not bound");
     if ((mask == nullptr) != (source == nullptr)) return fail(h, MRTS_EINVAL, "bind_mask_outputs: mask and source go together");

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "microrts_amd.h"   // mrts_sample_seg, MRTS_* limits
+
 // Phase stamps (tracing, experiment builds only: `make STAMPS=1`): each step
 // workgroup takes a row of g_stamp and writes wall_clock64() (100 MHz) at its
 // phase boundaries; mrts_debug_stamps (mrts_engine.hip) reads the rows back.
@@ -97,6 +99,7 @@ hipError_t mrts_engine_raw_obs(const EngineParams *p, hipStream_t s, int32_t *ra
 hipError_t mrts_engine_sample(const int32_t *mask, int n, int hw, int env0, uint64_t seed, uint32_t step, int64_t *act, hipStream_t s);
 hipError_t mrts_engine_sample_src(const int32_t *mask, const int32_t *src, int n, int hw, int env0, uint64_t seed, uint32_t step,
                                   int64_t *act, hipStream_t s);
+hipError_t mrts_engine_sample_src_group(const mrts_sample_seg *segs, int nseg, uint64_t seed, uint32_t step, hipStream_t s);
 hipError_t mrts_engine_render(const EngineParams *p, hipStream_t s, int game, int map, int size, uint8_t *rgb);
 size_t mrts_engine_lds_bytes(int HW, int W);
 size_t mrts_engine_bot_lds_bytes(int HW, int W);

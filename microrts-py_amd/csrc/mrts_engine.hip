@@ -1724,13 +1724,14 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sample(const int32_t* __restric
 // (32.7 -> 32.4 us, configs[1] 2 % slower).
 constexpr int SR_WAVES = 4;
 constexpr int SRC_ROWS = 4;   // source rows per round trip (8 and 16 measured slower, profiles/r04_ab/r04v)
-__global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n,
-                                                           int hw, int env0, uint64_t seed, uint32_t step,
-                                                           int64_t* __restrict__ act) {
-    __shared__ __attribute__((aligned(16))) int64_t s_out[SR_WAVES][64 * 7];
+// one block's 4 x 64 rows of one batch (k_sample_src: block = blockIdx.x; the grouped
+// launch: the block's index inside its segment)
+__device__ __forceinline__ void sample_src_block(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n, int hw,
+                                                 int env0, uint64_t seed, uint32_t step, int64_t* __restrict__ act, long long blk,
+                                                 int64_t (*s_out)[64 * 7]) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long rows = (long long)n * hw;
-    const long long row0 = ((long long)blockIdx.x * SR_WAVES + w) * 64;
+    const long long row0 = (blk * SR_WAVES + w) * 64;
     if (row0 >= rows) return;
     const int rb = (int)min(64ll, rows - row0);
     const bool in = lane < rb;
@@ -1780,6 +1781,33 @@ __global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __r
         __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(o4 + k));
     }
     if ((onel & 1) && lane == 0) ob[onel - 1] = s_out[w][onel - 1];
+}
+__global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src(const int32_t* __restrict__ mask, const int32_t* __restrict__ src, int n,
+                                                           int hw, int env0, uint64_t seed, uint32_t step,
+                                                           int64_t* __restrict__ act) {
+    __shared__ __attribute__((aligned(16))) int64_t s_out[SR_WAVES][64 * 7];
+    sample_src_block(mask, src, n, hw, env0, seed, step, act, blockIdx.x, s_out);
+}
+// Several batches (a mixed batch's size buckets) in one launch: segment k owns blocks
+// [end[k-1], end[k]); a block finds its segment with a scalar scan of the table.
+struct SampleSeg {
+    const int32_t* mask;
+    const int32_t* src;
+    int64_t* act;
+    int n, hw, env0;
+};
+struct SampleGroup {
+    SampleSeg seg[MRTS_SAMPLE_GROUP_MAX];
+    long long end[MRTS_SAMPLE_GROUP_MAX];
+    int nseg;
+};
+__global__ __launch_bounds__(64 * SR_WAVES) void k_sample_src_group(const SampleGroup g, uint64_t seed, uint32_t step) {
+    __shared__ __attribute__((aligned(16))) int64_t s_out[SR_WAVES][64 * 7];
+    const long long b = blockIdx.x;
+    int k = 0;
+    while (k + 1 < g.nseg && b >= g.end[k]) k++;
+    const SampleSeg& sg = g.seg[k];
+    sample_src_block(sg.mask, sg.src, sg.n, sg.hw, sg.env0, seed, step, sg.act, b - (k ? g.end[k - 1] : 0), s_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -1978,6 +2006,20 @@ hipError_t mrts_engine_sample_src(const int32_t* mask, const int32_t* src, int n
     if (rows == 0) return hipSuccess;
     const long long blocks = (rows + 64 * mrts::SR_WAVES - 1) / (64 * mrts::SR_WAVES);
     hipLaunchKernelGGL(mrts::k_sample_src, dim3((unsigned)blocks), dim3(64 * mrts::SR_WAVES), 0, s, mask, src, n, hw, env0, seed, step, act);
+    return hipGetLastError();
+}
+hipError_t mrts_engine_sample_src_group(const mrts_sample_seg* segs, int nseg, uint64_t seed, uint32_t step, hipStream_t s) {
+    mrts::SampleGroup g{};
+    long long blocks = 0;
+    for (int k = 0; k < nseg; k++) {
+        const mrts_sample_seg& q = segs[k];
+        g.seg[k] = mrts::SampleSeg{q.mask, q.source, q.actions, q.num_envs, q.hw, q.env0};
+        blocks += ((long long)q.num_envs * q.hw + 64 * mrts::SR_WAVES - 1) / (64 * mrts::SR_WAVES);
+        g.end[k] = blocks;
+    }
+    g.nseg = nseg;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(mrts::k_sample_src_group, dim3((unsigned)blocks), dim3(64 * mrts::SR_WAVES), 0, s, g, seed, step);
     return hipGetLastError();
 }
 hipError_t mrts_engine_render(const EngineParams* p, hipStream_t s, int game, int map, int size, uint8_t* rgb) {

@@ -73,6 +73,15 @@ class StepIO(ctypes.Structure):
 
 
 STEP_GROUP_MAX = 4
+
+
+class SampleSeg(ctypes.Structure):
+    """mrts_sample_seg: one batch of an mrts_sample_actions_src_group call."""
+    _fields_ = [("mask", P), ("source", P), ("num_envs", ctypes.c_int32), ("hw", ctypes.c_int32), ("env0", ctypes.c_int32),
+                ("actions", P)]
+
+
+SAMPLE_GROUP_MAX = 4
 GROUP_SEPARATE, GROUP_MERGE_FIT, GROUP_MERGE_ALL, GROUP_BOTS_FIRST = 0, 1, 2, 4
 
 # every entry point of include/microrts_amd.h: (restype, argtypes)
@@ -94,6 +103,7 @@ SIGNATURES = {
     "mrts_sample_actions": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]),
     "mrts_sample_actions_src": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                                ctypes.c_uint32, P]),
+    "mrts_sample_actions_src_group": (ctypes.c_int, [P, P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32]),
     "mrts_game_stats": (ctypes.c_int, [P, P, P]),
     "mrts_bind_mask_outputs": (ctypes.c_int, [P, P, P]),
     "mrts_set_bot_fusion": (ctypes.c_int, [P, ctypes.c_int32]),

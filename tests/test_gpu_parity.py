@@ -434,3 +434,56 @@ def test_parked_games_read_zero_in_mask_and_raw_kernels(eager):
     assert int(env._src[live].sum()) > 0 and int(raw[live].sum()) > 0
     assert int((m[live] == 3).sum()) == 0   # live rows rewritten by the mask kernel / eager masks
     env.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_grouped_source_sampler_equals_per_batch_calls(seed):
+    """mrts_sample_actions_src_group: 1-4 batches of random shapes (ragged row counts, map
+    sizes 4x4..24x24, any env0) in one launch == one mrts_sample_actions_src call per batch ==
+    the oracle's sampler, bit for bit."""
+    import ctypes
+
+    from gym_microrts import _native
+    from oracle_py import sample_actions
+
+    torch = _torch()
+    rng = np.random.default_rng(900 + seed)
+    nseg = int(rng.integers(1, 5))
+    segs, outs, refs, keep = [], [], [], []
+    for k in range(nseg):
+        n, hw, env0 = int(rng.integers(1, 40)), int(rng.choice([16, 37, 64, 100, 256, 576])), int(rng.integers(0, 5000))
+        m = (rng.random((n, hw, 78)) < 0.15).astype(np.int32)
+        m[:, ::3] = 0
+        src = (m.sum(-1) > 0).astype(np.int32)
+        m[:, :, 0] |= src
+        md, sd = torch.from_numpy(m).cuda(), torch.from_numpy(src).cuda()
+        out = torch.full((n, hw, 7), -1, dtype=torch.int64, device="cuda")
+        ref = torch.full((n, hw, 7), -2, dtype=torch.int64, device="cuda")
+        _native.check(_native.lib().mrts_sample_actions_src(torch.cuda.current_stream().cuda_stream, md.data_ptr(), sd.data_ptr(),
+                                                            n, hw, env0, ctypes.c_uint64(77 + seed), 11, ref.data_ptr()))
+        segs.append(_native.SampleSeg(md.data_ptr(), sd.data_ptr(), n, hw, env0, out.data_ptr()))
+        outs.append(out)
+        refs.append((ref, m, env0))
+        keep += [md, sd]
+    arr = (_native.SampleSeg * nseg)(*segs)
+    _native.check(_native.lib().mrts_sample_actions_src_group(torch.cuda.current_stream().cuda_stream, arr, nseg,
+                                                              ctypes.c_uint64(77 + seed), 11))
+    for out, (ref, m, env0) in zip(outs, refs):
+        assert torch.equal(out, ref)
+        np.testing.assert_array_equal(out.cpu().numpy(), sample_actions(m, 77 + seed, 11, env0=env0))
+
+
+def test_grouped_source_sampler_refuses_bad_groups():
+    from gym_microrts import _native
+
+    torch = _torch()
+    lib, st = _native.lib(), torch.cuda.current_stream().cuda_stream
+    m = torch.zeros((2, 16, 78), dtype=torch.int32, device="cuda")
+    s = torch.zeros((2, 16), dtype=torch.int32, device="cuda")
+    a = torch.zeros((2 * 16 * 7 + 2,), dtype=torch.int64, device="cuda")
+    ok = _native.SampleSeg(m.data_ptr(), s.data_ptr(), 2, 16, 0, a.data_ptr())
+    assert lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 1)(ok), 0, 1, 0) == -1   # MRTS_EINVAL
+    assert lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 5)(*[ok] * 5), 5, 1, 0) == -1   # MRTS_EINVAL
+    bad = _native.SampleSeg(m.data_ptr(), s.data_ptr(), 2, 16, 0, a.data_ptr() + 8)   # actions not 16-byte aligned
+    assert lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 2)(ok, bad), 2, 1, 0) == -1   # MRTS_EINVAL
+    assert lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 1)(ok), 1, 1, 0) == 0
