@@ -169,7 +169,10 @@ def test_fullsize_headline_8192_staggered_2000_ticks():
     same(g.reset(), o.reset(), "reset obs", -1)
     plan = bench.stagger_plan(n // 2, 2000)
     ends = 0
-    for s in range(2100):
+    ticks = int(os.environ.get("MRTS_SOAK_TICKS", "2100"))   # a soak run: more episodes back to back
+    for s in range(ticks):
+        if s % 500 == 0:
+            print(f"headline lock-step: tick {s} / {ticks}", flush=True)
         g.get_action_mask()
         _native.check(bench.sample(lib, "src", g._mask, g._src, n, hw, 0, seed, s, act), None, "sample")
         og, _, dg, ig = g.step(act)
@@ -181,7 +184,7 @@ def test_fullsize_headline_8192_staggered_2000_ticks():
             g.reset_games(plan[s])
             for k in plan[s]:
                 o.reset_game(k, 0)
-        if s % 50 == 0 or s == 2099:
+        if s % 50 == 0 or s == ticks - 1:
             same(og, o.encode(o.raw_obs()), "obs", s)
             full = o.get_action_mask_full()
             same(g.get_action_mask(), full[:, :, 1:], "mask", s)
