@@ -41,6 +41,8 @@ def _full_rollout(map_path, nsp, nbot, bot, steps, max_steps, partial_obs=False,
     same(g.reset(), o.reset(), "reset obs", -1)
     resets = 0
     for s in range(steps):
+        if s % 500 == 0:
+            print(f"{map_path} {nsp}+{nbot} {bot}: step {s} / {steps}", flush=True)
         mg, mo = g.get_action_mask(), o.get_action_mask()
         same(mg, mo, "mask", s)
         same(g.source_unit_mask, o.source_unit_mask, "source mask", s)
@@ -67,8 +69,9 @@ def test_fullsize_selfplay_8192_basesWorkers16x16():
 
 @pytest.mark.timeout(900)
 def test_fullsize_coacai_1024():
-    """configs[1]: 1024 envs vs device coacAI."""
-    _full_rollout("maps/16x16/basesWorkers16x16.xml", 0, 1024, "coacAI", steps=500, max_steps=400)
+    """configs[1]: 1024 envs vs device coacAI (MRTS_SOAK_TICKS: a longer soak run)."""
+    _full_rollout("maps/16x16/basesWorkers16x16.xml", 0, 1024, "coacAI", steps=int(os.environ.get("MRTS_SOAK_TICKS", "500")),
+                  max_steps=400)
 
 
 @pytest.mark.timeout(900)
