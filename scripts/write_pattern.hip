@@ -37,6 +37,10 @@
 //           into registers, parked in LDS when its step comes, and the chunk's words are built from
 //           LDS (cell + 4 neighbours) -- what a logic / emit split's emit kernel would have to do
 //   mode 32 as 31 with D = 16, mode 33 as 31 on 512 workgroups
+//   mode 34 wave-private emit proxy: each wave walks the window in 1 KB chunks; lane L loads the
+//           state of cell c0 - 16 + L (the chunk's cells and their row neighbours, one int4 per
+//           lane) D = 16 chunks ahead in a statically unrolled ring (no register rotation, no
+//           barrier); the words are built with cross-lane reads.  Mode 35: D = 24, mode 36: D = 8
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/write_pattern scripts/write_pattern.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -130,6 +134,59 @@ __global__ __launch_bounds__(256) void k_emit_pipe(int* obs, int* mask, const in
     __shared__ int lw[HW];   // the step's game, one word per cell
     emit_pipe<D, P, false>(obs, state, G, salt, lw);
     emit_pipe<D, CH, true>(mask, state, G, salt, lw);
+}
+
+template <int D, int WIDTH, bool NB>
+__device__ __forceinline__ void emit_wave(int* out, const int4* __restrict__ state, int G, int salt) {
+    constexpr int PER = NV * HW * WIDTH / 4;   // 16-B stores per game
+    const int lane = threadIdx.x & 63;
+    const unsigned nw = gridDim.x * 4u, gw = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const unsigned nch = ((unsigned)G * PER + 63) / 64;   // 1 KB chunks
+    auto cell_of = [&](unsigned j, unsigned& g, int& c0) {   // chunk j: its game and first cell
+        const unsigned k0 = j * 64u;
+        g = min(k0 / PER, (unsigned)G - 1);
+        c0 = (int)((4 * (k0 - g * PER) / WIDTH) & (HW - 1));
+    };
+    auto load = [&](unsigned j) {
+        unsigned g;
+        int c0;
+        cell_of(min(j, nch - 1), g, c0);
+        return state[(size_t)g * HW + min(max(c0 - 16 + lane, 0), HW - 1)];
+    };
+    int4 ring[D];
+#pragma unroll
+    for (int d = 0; d < D; d++) ring[d] = load(gw + d * nw);
+    for (unsigned j0 = gw; j0 < nch; j0 += D * nw) {
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const unsigned j = min(j0 + d * nw, nch - 1);   // past the end: rewrites the last chunk (same words)
+            const int4 u = ring[d];
+            ring[d] = load(j0 + d * nw + D * nw);
+            {
+                unsigned g;
+                int c0;
+                cell_of(j, g, c0);
+                const int word = (u.x & 15) | ((u.x >> 4 & 3) << 4) | ((u.z & 7) << 8) | (u.w & 0xff) << 12;
+                const unsigned k = j * 64u + lane, w0 = 4 * (k - g * PER), c2 = w0 / WIDTH, ch = w0 - c2 * WIDTH;
+                const int c = (int)(c2 & (HW - 1)), rel = min(max(c - c0 + 16, 0), 63);
+                int acc = __shfl(word, rel);
+                if (NB) {
+                    acc ^= __shfl(word, max(rel - 16, 0)) << 1;
+                    acc ^= __shfl(word, min(rel + 1, 63)) << 2;
+                    acc ^= __shfl(word, min(rel + 16, 63)) << 3;
+                    acc ^= __shfl(word, max(rel - 1, 0)) << 4;
+                }
+                v4i v;
+                for (int q = 0; q < 4; q++) v[q] = ((acc >> ((ch + q) & 31)) & 1) ^ salt;
+                if (k < (unsigned)G * PER) *reinterpret_cast<v4i*>(out + 4 * (size_t)k) = v;
+            }
+        }
+    }
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_emit_wave(int* obs, int* mask, const int4* __restrict__ state, int G, int salt) {
+    emit_wave<D, P, false>(obs, state, G, salt);
+    emit_wave<D, CH, true>(mask, state, G, salt);
 }
 
 __global__ __launch_bounds__(256) void k_pattern(int mode, int* obs, int* mask, int G, int salt) {
@@ -240,7 +297,7 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[34] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
+    const char* names[37] = {"phaseB_4KB_iter", "wave_contiguous_quarter", "wave_local_cells", "grid_stride_fill",
                              "grid_stride_constant", "grid_stride_nontemporal", "phaseB_constant", "hipMemsetD32",
                              "grid_stride_256wg", "grid_stride_512wg", "grid_stride_1024wg", "phaseB_2waves", "phaseB_1wave",
                              "grid_stride_256wg_nt", "games_256_persistent", "games_1024_persistent", "games_512_persistent",
@@ -248,9 +305,14 @@ int main() {
                              "phaseB_mask_first", "phaseB_game_swizzle", "games_256_block", "games_512_block",
                              "games_1024_block", "games_128_block", "block_fill_256wg", "emit_proxy_256wg",
                              "emit_proxy_512wg", "emit_proxy_1792wg", "emit_pipe_D8_256wg",
-                             "emit_pipe_D16_256wg", "emit_pipe_D8_512wg"};
+                             "emit_pipe_D16_256wg", "emit_pipe_D8_512wg", "emit_wave_D16_256wg",
+                             "emit_wave_D24_256wg", "emit_wave_D8_256wg"};
     auto launch = [&](int mode, int grid, int i) {
-        if (mode >= 31) {
+        if (mode >= 34) {
+            if (mode == 34) hipLaunchKernelGGL(k_emit_wave<16>, dim3(256), dim3(256), 0, 0, obs, mask, (const int4*)state, G, i);
+            if (mode == 35) hipLaunchKernelGGL(k_emit_wave<24>, dim3(256), dim3(256), 0, 0, obs, mask, (const int4*)state, G, i);
+            if (mode == 36) hipLaunchKernelGGL(k_emit_wave<8>, dim3(256), dim3(256), 0, 0, obs, mask, (const int4*)state, G, i);
+        } else if (mode >= 31) {
             if (mode == 32)
                 hipLaunchKernelGGL(k_emit_pipe<16>, dim3(256), dim3(256), 0, 0, obs, mask, (const int4*)state, G, i);
             else
@@ -266,7 +328,7 @@ int main() {
         }
     };
     for (int round = 0; round < 3; round++) {
-        for (int mode = 0; mode < 34; mode++) {
+        for (int mode = 0; mode < 37; mode++) {
             const int grid = (mode >= 3 && mode <= 5) ? 256 * 7 : (mode == 8 || mode == 13 || mode == 14 || mode == 23 || mode == 27) ? 256
                            : (mode == 9 || mode == 16 || mode == 24) ? 512 : (mode == 10 || mode == 15 || mode == 25) ? 1024
                            : mode == 26 ? 128 : G;
