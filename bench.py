@@ -206,11 +206,17 @@ def run_mixed(args, rank, world, dev):
         for e in env.envs:
             e.kernel_events = ev.setdefault(e.height, {}) if rec else None
         if grouped_sampler:
+            if rec:
+                s0e, s1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0e.record()
             segs = (_native.SampleSeg * len(env.envs))(*[
                 _native.SampleSeg(m.data_ptr(), e.source_unit_mask.data_ptr(), e.num_envs, e.height * e.width, rank * e.num_envs,
                                   a.data_ptr()) for e, m, a in zip(env.envs, masks, acts)])
             _native.check(lib.mrts_sample_actions_src_group(torch.cuda.current_stream().cuda_stream, segs, len(env.envs), seed, s),
                           None, "sample_group")
+            if rec:
+                s1e.record()
+                ev.setdefault("sample", []).append((s0e, s1e))
         else:
             for e, m, a in zip(env.envs, masks, acts):
                 _native.check(sample(lib, args.sampler, m, e.source_unit_mask, e.num_envs, e.height * e.width, rank * e.num_envs,
@@ -260,6 +266,11 @@ def run_mixed(args, rank, world, dev):
     stats["sampler_launches_per_step"] = 1 if grouped_sampler else len(env.envs)
     if ev.get("all"):
         stats["step_all_buckets_ms"] = float(np.mean([a.elapsed_time(b) for a, b in ev["all"]]))
+    if ev.get("sample"):   # the grouped sampler: source read + actions written + the source rows' mask rows
+        src = sum(int(e.source_unit_mask.sum().item()) for e in env.envs)
+        sb = sum(e.num_envs * e.height * e.width * (4 + 7 * 8) for e in env.envs) + src * 78 * 4
+        sms = float(np.mean([a.elapsed_time(b) for a, b in ev["sample"]]))
+        stats["sampler_group"] = {"avg_ms": round(sms, 4), "bytes": sb, "gbs": round(sb / (sms * 1e-3) / 1e9, 1)}
     return elapsed, {}, env.error_flags(), 256, sum(e._n_games() for e in env.envs), env.num_envs, 29, 0, stats
 
 
