@@ -487,3 +487,33 @@ def test_grouped_source_sampler_refuses_bad_groups():
     bad = _native.SampleSeg(m.data_ptr(), s.data_ptr(), 2, 16, 0, a.data_ptr() + 8)   # actions not 16-byte aligned
     assert lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 2)(ok, bad), 2, 1, 0) == -1   # MRTS_EINVAL
     assert lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 1)(ok), 1, 1, 0) == 0
+
+
+def test_grouped_source_sampler_empty_segment():
+    """A zero-env segment between two others owns no block: the neighbours' actions are still
+    their own calls' (the block -> segment scan skips it)."""
+    import ctypes
+
+    from gym_microrts import _native
+
+    torch = _torch()
+    lib, st = _native.lib(), torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(5)
+    segs, outs, refs, keep = [], [], [], []
+    for n, hw in ((3, 64), (0, 256), (5, 100)):
+        m = (rng.random((max(n, 1), hw, 78)) < 0.2).astype(np.int32)
+        src = (m.sum(-1) > 0).astype(np.int32)
+        m[:, :, 0] |= src
+        md, sd = torch.from_numpy(m).cuda(), torch.from_numpy(src).cuda()
+        out = torch.full((max(n, 1), hw, 7), -1, dtype=torch.int64, device="cuda")
+        ref = out.clone()
+        if n:
+            _native.check(lib.mrts_sample_actions_src(st, md.data_ptr(), sd.data_ptr(), n, hw, 0, ctypes.c_uint64(3), 4,
+                                                      ref.data_ptr()))
+        segs.append(_native.SampleSeg(md.data_ptr(), sd.data_ptr(), n, hw, 0, out.data_ptr()))
+        outs.append(out)
+        refs.append(ref)
+        keep += [md, sd]
+    _native.check(lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 3)(*segs), 3, ctypes.c_uint64(3), 4))
+    for out, ref in zip(outs, refs):
+        assert torch.equal(out, ref)   # the empty segment's buffer untouched (-1 both)
