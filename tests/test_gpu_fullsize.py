@@ -76,8 +76,9 @@ def test_fullsize_coacai_1024():
 
 @pytest.mark.timeout(900)
 def test_fullsize_partial_obs_4096():
-    """configs[3]'s env: partial_obs (31 planes), 4096 envs."""
-    _full_rollout("maps/16x16/basesWorkers16x16.xml", 4096, 0, "passiveAI", steps=120, max_steps=100, partial_obs=True)
+    """configs[3]'s env: partial_obs (31 planes), 4096 envs (MRTS_SOAK_TICKS: a longer soak run)."""
+    _full_rollout("maps/16x16/basesWorkers16x16.xml", 4096, 0, "passiveAI", steps=int(os.environ.get("MRTS_SOAK_TICKS", "120")),
+                  max_steps=100, partial_obs=True)
 
 
 @pytest.mark.timeout(900)
