@@ -211,8 +211,9 @@ def test_fullsize_mixed_buckets_bench_split_8192():
     24x24 basesWorkers (bench.MIXED), each bucket half selfplay, a quarter vs device
     workerRushAI, a quarter vs device coacAI -- stepped by one mrts_step_group call with
     the default merge-fit | bots-first policy (8x8 and 16x16 share one 256-lane launch
-    with a segment table, 24x24 keeps its own), the device Philox sampler on each
-    bucket's eager masks, and bench.preroll's staggered restarts over the first 100 ticks.
+    with a segment table, 24x24 keeps its own), the device Philox sampler on every
+    bucket's eager masks in one grouped launch (as the bench samples), and bench.preroll's
+    staggered restarts over the first 100 ticks.
     max_steps 100 over 210 ticks, so every game also reaches its time-limit auto-reset.  One oracle per
     bucket (ovec_bench_steps: the oracle's identical C sampler + step): raw rewards and
     dones every tick, the whole obs / mask / source tensors every 10 ticks."""
@@ -226,7 +227,8 @@ def test_fullsize_mixed_buckets_bench_split_8192():
     from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
     from oracle_py import OracleVecEnv
 
-    n, seed, max_steps, ticks = 8192, 5, 100, 210
+    n, seed, max_steps = 8192, 5, 100
+    ticks = int(os.environ.get("MRTS_SOAK_TICKS", "210"))   # a soak run: more episodes back to back
     buckets, spec = [], []
     for m, frac in bench.MIXED:
         nb = int(n * frac) // 4 * 4
@@ -252,10 +254,15 @@ def test_fullsize_mixed_buckets_bench_split_8192():
     plans = [bench.stagger_plan(e._n_games(), max_steps) for e in env.envs]
     ends = np.zeros(3, int)
     for s in range(ticks):
+        if s % 500 == 0:
+            print(f"configs[4] lock-step: tick {s} / {ticks}", flush=True)
         masks = env.get_action_mask()
-        for e, mk, a in zip(env.envs, masks, acts):
-            _native.check(bench.sample(lib, "src", mk, e.source_unit_mask, e.num_envs, e.height * e.width, 0, seed, s, a),
-                          None, "sample")
+        # the bench's stand-in policy: every bucket in one mrts_sample_actions_src_group launch
+        segs = (_native.SampleSeg * 3)(*[_native.SampleSeg(mk.data_ptr(), e.source_unit_mask.data_ptr(), e.num_envs,
+                                                           e.height * e.width, 0, a.data_ptr())
+                                         for e, mk, a in zip(env.envs, masks, acts)])
+        _native.check(lib.mrts_sample_actions_src_group(torch.cuda.current_stream().cuda_stream, segs, 3, seed, s), None,
+                      "sample_group")
         obs, rew, done, infos = env.step(acts)
         for k, (e, o) in enumerate(zip(env.envs, orc)):
             _, ro, do = o.bench_steps(1, seed, s)
