@@ -20,6 +20,29 @@ def maps_root():
     return MAPS
 
 
+ONE_F32 = 0x3f800000   # 1.0f as stored bits
+
+
+def obs_bits_equal(gpu, host):
+    """Bit-level obs parity.  `host` is the oracle's int32 one-hot; an int32 `gpu`
+    tensor must equal it, a float32 one must hold exactly 0x3f800000 (1.0f) where
+    the one-hot is 1 and 0x00000000 (+0.0f) where it is 0 -- the bits the bench's
+    float kernels store (mrts_engine.hip stream_obs: ONE, and the unaligned
+    fallback's cast)."""
+    import numpy as np
+    import torch
+
+    h = torch.from_numpy(np.ascontiguousarray(host, dtype=np.int32)).to(gpu.device)
+    if gpu.dtype == torch.int32:
+        return torch.equal(gpu, h)
+    assert gpu.dtype == torch.float32, gpu.dtype
+    assert bool(((h == 0) | (h == 1)).all()), "oracle obs is not one-hot"
+    return torch.equal(gpu.view(torch.int32), h * ONE_F32)
+
+
+OBS_DTYPES = ("float32", "int32")   # the bench's dtype first
+
+
 def gpu_available():
     try:
         import torch

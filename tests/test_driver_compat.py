@@ -147,6 +147,7 @@ def test_reference_drivers_import_unmodified(tmp_path, script, flag):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
 def test_ppo_gridnet_wrapper_stack_on_device(compat, tmp_path):
     """ppo_gridnet.py:364-389: env -> VecEnvWrapper subclass -> VecMonitor; masks through
     both wrappers (:466), host int64 actions (:475), info["episode"] when an env hits

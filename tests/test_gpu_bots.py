@@ -9,7 +9,7 @@ import pytest
 
 from conftest import MAPS
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 
 BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "randomAI", "POWorkerRush", "POLightRush",
         "POHeavyRush", "PORangedRush"]

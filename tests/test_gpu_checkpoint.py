@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
 
 

@@ -16,7 +16,7 @@ import pytest
 
 from conftest import REPO
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 
 NVEC = [6, 4, 4, 4, 4, 7, 49]
 

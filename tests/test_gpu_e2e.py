@@ -10,7 +10,7 @@ import os
 
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

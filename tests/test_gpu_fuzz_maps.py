@@ -12,7 +12,7 @@ import pytest
 from random_maps import write_random_map
 from test_gpu_bots import BOTS, lockstep
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 SEEDS = int(os.environ.get("MRTS_FUZZ_SEEDS", "12"))
 FIRST = int(os.environ.get("MRTS_FUZZ_FIRST", "0"))
 

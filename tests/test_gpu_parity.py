@@ -13,9 +13,9 @@ import numpy as np
 import pytest
 
 import kat
-from conftest import MAPS
+from conftest import MAPS, obs_bits_equal
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 
 
 def _torch():
@@ -67,17 +67,21 @@ def test_kat_reward():
 
 
 def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_tensors=False, partial_obs=False,
-             eager_masks=True):
-    """Lock-step GPU vs oracle rollout; compares masks, obs, rewards, dones."""
+             eager_masks=True, obs_dtype="int32"):
+    """Lock-step GPU vs oracle rollout; compares masks, obs, rewards, dones.  With
+    return_tensors, `obs_dtype` picks the device obs (float32 obs are bit-compared:
+    1.0f / +0.0f against the oracle's one-hot)."""
     from oracle_py import sample_actions
 
     torch = _torch()
     g = make_gpu_env(nsp, nbot, map_path, max_steps, return_tensors=return_tensors,
-                     obs_dtype=torch.int32 if return_tensors else None, partial_obs=partial_obs, eager_masks=eager_masks)
+                     obs_dtype=getattr(torch, obs_dtype) if return_tensors else None, partial_obs=partial_obs,
+                     eager_masks=eager_masks)
     o = make_oracle(nsp, nbot, map_path, max_steps, partial_obs=partial_obs)
-    og = np.asarray(g.reset().cpu() if return_tensors else g.reset())
-    oo = o.reset()
-    np.testing.assert_array_equal(og, oo)
+    if return_tensors:
+        assert obs_bits_equal(g.reset(), o.reset()), "reset obs"
+    else:
+        np.testing.assert_array_equal(g.reset(), o.reset())
     rng = np.random.default_rng(seed)
     n, hw = g.num_envs, g.height * g.width
     nvec = np.array([6, 4, 4, 4, 4, 7, 49])
@@ -99,8 +103,10 @@ def _rollout(map_path, nsp, nbot, max_steps, steps, seed, mode="masked", return_
         obs_g, rew_g, done_g, info_g = g.step(torch.from_numpy(a).to(g.device) if return_tensors else a)
         obs_o, rew_o, done_o, info_o = o.step(a)
         if return_tensors:
-            obs_g, rew_g, done_g = obs_g.cpu().numpy(), rew_g.cpu().numpy(), done_g.cpu().numpy()
-        np.testing.assert_array_equal(obs_g, obs_o, err_msg=f"obs step {s}")
+            assert obs_bits_equal(obs_g, obs_o), f"obs step {s}"
+            rew_g, done_g = rew_g.cpu().numpy(), done_g.cpu().numpy()
+        else:
+            np.testing.assert_array_equal(obs_g, obs_o, err_msg=f"obs step {s}")
         np.testing.assert_array_equal(np.array([i["raw_rewards"] for i in info_g]), np.array([i["raw_rewards"] for i in info_o]),
                                       err_msg=f"raw rewards step {s}")
         if return_tensors:
@@ -155,6 +161,21 @@ def test_partial_obs_tensor_path():
 
 def test_tensor_path_bit_exact():
     _rollout("maps/16x16/basesWorkers16x16.xml", 32, 0, 300, 300, seed=3, return_tensors=True)
+
+
+@pytest.mark.parametrize("partial_obs", [False, True])
+@pytest.mark.parametrize("map_path,nsp,nbot", [
+    ("maps/16x16/basesWorkers16x16.xml", 32, 8),        # HW * P % 4 == 0: the 16-byte store path
+    ("maps/4x4/baseTwoWorkers4x4.xml", 16, 16),         # the smallest map (16-byte path)
+    ("maps/9x13/basesWorkersWalls9x13.xml", 16, 8),     # 117 * P odd: the unaligned per-element fallback
+    ("maps/15x15/basesWorkersWalls15x15.xml", 8, 4),    # 225 * P odd, walls
+])
+def test_float32_obs_rollout_bit_exact(map_path, nsp, nbot, partial_obs):
+    """The bench's obs dtype over a whole rollout: float32 obs
+    from k_step<.., P, float, ..> -- the 16-byte stream_obs path and the unaligned
+    fallback's cast (mrts_engine.hip stream_obs) -- bit-compared with the oracle's
+    one-hot as 1.0f / +0.0f every step, with bot envs, auto-resets and fog."""
+    _rollout(map_path, nsp, nbot, 150, 400, seed=21, return_tensors=True, partial_obs=partial_obs, obs_dtype="float32")
 
 
 @pytest.mark.parametrize("partial_obs", [False, True])

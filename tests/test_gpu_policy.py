@@ -22,7 +22,7 @@ import pytest
 
 from conftest import MAPS
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
 MAP = "maps/16x16/basesWorkers16x16A.xml"

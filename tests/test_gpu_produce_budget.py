@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
 UP, RIGHT, DOWN, LEFT = 0, 1, 2, 3
 WORKER, LIGHT, HEAVY, RANGED = 3, 4, 5, 6

@@ -10,7 +10,7 @@ import pytest
 from random_maps import write_random_map
 from test_gpu_bots import lockstep
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 BOTS = ["coacAI", "workerRushAI", "lightRushAI", "randomBiasedAI", "POWorkerRush", "PORangedRush", "POHeavyRush",
         "POLightRush", "randomAI", "passiveAI"]
 

@@ -13,7 +13,7 @@ import pytest
 
 from conftest import MAPS
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 
 
 @pytest.mark.parametrize("map_path,nsp,nbot", [

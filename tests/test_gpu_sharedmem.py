@@ -19,6 +19,7 @@ def test_sharedmem_requires_one_map():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("map_path,nsp,bots", [("maps/16x16/basesWorkers16x16.xml", 16, ["coacAI", "workerRushAI"] * 4),
                                                ("maps/10x10/basesTwoWorkers10x10.xml", 8, ["passiveAI", "lightRushAI"])])
 def test_sharedmem_lockstep_vs_oracle(map_path, nsp, bots):

@@ -14,7 +14,7 @@ import pytest
 
 from conftest import MAPS
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 
 CYCLE = ["maps/8x8/basesWorkers8x8.xml", "maps/16x16/basesWorkers16x16A.xml", "maps/10x10/basesTwoWorkers10x10.xml",
          "maps/16x16/melee16x16Mixed8.xml", "maps/24x24/basesWorkers24x24.xml", "maps/16x16/basesWorkers16x16C.xml",

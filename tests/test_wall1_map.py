@@ -102,6 +102,7 @@ def test_capi_loader_accepts_wall1():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("partial_obs", [False, True])
 def test_gpu_reset_matches_reference_vectors(partial_obs):
     from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
@@ -125,6 +126,7 @@ def test_gpu_reset_matches_reference_vectors(partial_obs):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("bot_fusion", [True, False])
 @pytest.mark.parametrize("partial_obs", [False, True])
 def test_gpu_lockstep_wall1(bot_fusion, partial_obs):
@@ -136,6 +138,7 @@ def test_gpu_lockstep_wall1(bot_fusion, partial_obs):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
 def test_gpu_lockstep_wall1_adversarial():
     """unmasked agent actions on the walled map (moves into walls, produce into walls)"""
     from test_gpu_bots import BOTS, lockstep
