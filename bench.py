@@ -75,10 +75,13 @@ def parse(argv=None):
                          "the host -- the env shards exchange no data, so nothing on the data path needs RCCL and an RCCL "
                          "init or topology problem cannot cost the scaling curve; nccl = RCCL over xGMI (each rank "
                          "synchronises its own device first either way)")
-    ap.add_argument("--rank-timeout", type=float, default=900.0,
+    ap.add_argument("--rank-timeout", type=float, default=None,
                     help="seconds: a self-launched parent terminates every rank and exits 124 when they have not all "
                          "exited by then (or STRAGGLE_S after rank 0 exited); each rank also exits 124 by itself "
-                         "after this long, so a hang under an external launcher ends too (0 = no deadline)")
+                         "after this long, so a hang under an external launcher ends too.  Default: derived from the "
+                         "requested work (rank_deadline: 900 s + 50 ms per pre-roll / warm-up / timed tick per seed, "
+                         "about 100x the real tick time); the value in force is in the line's window.rank_timeout_s. "
+                         "A longer run than that needs a larger value, or 0 = no deadline")
     ap.add_argument("--bucket-streams", type=int, default=0, choices=[0, 1],
                     help="mixed workload: 1 = each size bucket on its own HIP stream (concurrent), 0 = back to back")
     ap.add_argument("--group-policy", default="default",
@@ -90,7 +93,19 @@ def parse(argv=None):
                          "mrts_sample_actions_src_group launch, 0 = one launch per bucket (same actions)")
     ap.add_argument("--dump", default=None,
                     help="save each rank's final obs / masks / raw rewards / dones to DUMP.rank<r>.npz (shard tests)")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.rank_timeout is None:
+        a.rank_timeout = rank_deadline(a)
+    return a
+
+
+def rank_deadline(a):
+    """--rank-timeout's default: 900 s of start-up (torch import, rendezvous, env build,
+    the CPU-side cpu_baseline is rank 0 at N=1 only) plus 50 ms per tick the run asks
+    for -- pre-roll (max_steps by default), warm-up and timed steps, for every seed.
+    A tick takes about 0.2-0.5 ms, so only a hang reaches it."""
+    pre = a.max_steps if a.preroll < 0 else a.preroll
+    return 900.0 + 0.05 * max(1, a.seeds) * (pre + a.warmup + a.steps)
 
 
 # BASELINE.json configs as bench workloads: (map, selfplay envs, bot envs, bot, partial_obs).
@@ -814,6 +829,7 @@ def main(argv=None):
         }
         stats["per_rank"] = per_rank
         if world > 1:
+            stats["rank_timeout_s"] = args.rank_timeout
             el = [p["elapsed_s"] for p in per_rank]
             stats["per_rank_spread"] = round(max(el) / min(el), 4)   # slowest / fastest rank
         if args.workload != "selfplay":

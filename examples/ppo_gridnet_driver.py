@@ -92,10 +92,25 @@ class GridNet(nn.Module):
             if layer in self.REFERENCE_NAMES:
                 name = f"{self.REFERENCE_NAMES[layer]}.{field}"
                 t = torch.as_tensor(np.asarray(v))
-                assert own[name].shape == t.shape, (k, tuple(t.shape), tuple(own[name].shape))
+                if own[name].shape != t.shape:
+                    raise ValueError(f"{k}: shape {tuple(t.shape)}, this GridNet's {name} is {tuple(own[name].shape)}")
                 own[name] = t
                 done.append(k)
         self.load_state_dict(own)
+        return done
+
+    # what a policy needs to act: the encoder and the actor (the critic is optional --
+    # the trimmed fixture omits it, a full agent_sota.pt state_dict carries it)
+    POLICY_NAMES = [f"{layer}.{f}" for layer in ("encoder.1", "encoder.4", "actor.0", "actor.2") for f in ("weight", "bias")]
+
+    def load_reference_policy(self, tensors):
+        """load_reference_state, then require every encoder / actor tensor: a state_dict
+        missing one raises ValueError (not an assert, so it holds under python -O).
+        Critic tensors are accepted as extras.  Returns the names loaded."""
+        done = self.load_reference_state(tensors)
+        missing = [k for k in self.POLICY_NAMES if k not in done]
+        if missing:
+            raise ValueError(f"policy state_dict lacks {missing}")
         return done
 
     def forward(self, obs):
@@ -329,10 +344,10 @@ def evaluate(ai="", num_steps=256, total_timesteps=1000000, agent_model_path=SOT
     n, hw = envs.num_envs, envs.height * envs.width
     h, w, planes = envs.observation_space.shape
     agent, agent2 = GridNet(planes, h, w).to(dev), GridNet(planes, h, w).to(dev)
-    assert len(agent.load_reference_state(load_weights(agent_model_path))) == 8
+    agent.load_reference_policy(load_weights(agent_model_path))
     agent.eval()
     if not ai:
-        assert len(agent2.load_reference_state(load_weights(agent2_model_path))) == 8
+        agent2.load_reference_policy(load_weights(agent2_model_path))
         agent2.eval()
     num_updates = total_timesteps // (n * num_steps)
     next_obs = torch.Tensor(envs.reset()).to(dev)

@@ -258,11 +258,13 @@ int mrts_render(mrts_vec *h, void *stream, int32_t env, uint8_t *rgb, int32_t si
  * mirrors -- copied into / out of a caller device buffer of mrts_state_bytes(h)
  * bytes (256-byte aligned).  mrts_save_state synchronises the stream.
  * mrts_load_state restores a snapshot of the same configuration and map table
- * into this handle -- same env split, obs layout, game offset, bots (both players)
- * and map templates, checked by a fingerprint in the snapshot's header; MRTS_EINVAL
+ * into this handle -- same env split, obs layout, game offset, max_steps, bots (both
+ * players) and map templates, checked by a fingerprint in the snapshot's header; MRTS_EINVAL
  * otherwise, before anything but the fixed header is read -- and writes the restored state's obs
  * into `obs` (and its next-tick masks into the bound mask outputs), as mrts_reset
- * does for a fresh state; stepping on from it repeats the saved run bit for bit. */
+ * does for a fresh state; stepping on from it repeats the saved run bit for bit.
+ * The reward weights and shaping flag (mrts_set_reward_weight) are host settings the
+ * caller may change between steps: they are not in the snapshot and not checked. */
 size_t mrts_state_bytes(const mrts_vec *h);
 int mrts_save_state(mrts_vec *h, void *stream, void *dst);
 int mrts_load_state(mrts_vec *h, void *stream, const void *src, void *obs);

@@ -749,7 +749,7 @@ struct StateHeader {
     uint64_t config;   // config_fingerprint
 };
 const uint32_t kStateMagic = 0x4d525453u;   // "MRTS"
-const uint32_t kStateVersion = 2;
+const uint32_t kStateVersion = 3;
 size_t state_header_bytes(const mrts_vec *h) {
     return align256(sizeof(StateHeader) + (size_t)h->ngames * (sizeof(int32_t) + 1));
 }
@@ -762,12 +762,15 @@ struct Fnv {
     void i32(int32_t x) { bytes(&x, sizeof x); }
 };
 // FNV-1a over everything a workspace copy would carry in besides the game states:
-// env split, obs layout, global game offset (bot RNG streams), the bots of every bot
-// env (both players), the map table's capacity and every map template (size,
-// resources, walls, unit records)
+// env split, obs layout, global game offset (bot RNG streams), the time limit, the
+// bots of every bot env (both players), the map table's capacity and every map
+// template (size, resources, walls, unit records).  Not the reward weights / shaping:
+// the caller may reassign those between steps (vec_env.py reads reward_weight every step).
 uint64_t config_fingerprint(const mrts_vec *h) {
     Fnv f;
-    for (int32_t x : {h->nsp, h->nbot, h->partial_obs, h->obs_float, h->game_offset, h->map_capacity, h->W, h->H}) f.i32(x);
+    for (int32_t x : {h->nsp, h->nbot, h->partial_obs, h->obs_float, h->game_offset, h->map_capacity, h->W, h->H,
+                      h->max_steps})
+        f.i32(x);
     f.i32((int32_t)h->bot_ai.size());
     f.bytes(h->bot_ai.data(), h->bot_ai.size() * sizeof(int32_t));
     f.i32((int32_t)h->bot_ai0.size());
@@ -819,17 +822,18 @@ int mrts_load_state(mrts_vec *h, void *stream, const void *src, void *obs) {
     if (sh.ngames != h->ngames || sh.HW != h->HW || sh.nmaps != (int32_t)h->maps.size() || sh.total != (uint64_t)h->total)
         return fail(h, MRTS_EINVAL, "load_state: the snapshot belongs to another configuration or map table");
     if (sh.config != config_fingerprint(h))
-        return fail(h, MRTS_EINVAL, "load_state: the snapshot belongs to another configuration (bots, maps, obs layout "
-                                    "or game offset differ)");
+        return fail(h, MRTS_EINVAL, "load_state: the snapshot belongs to another configuration (bots, maps, obs layout, "
+                                    "game offset or max_steps differ)");
     std::vector<unsigned char> hdr(state_header_bytes(h), 0);
     e = hipMemcpyAsync(hdr.data(), src, hdr.size(), hipMemcpyDeviceToHost, s);
     if (!e) e = hipStreamSynchronize(s);
     if (e) return hip_fail(h, e, "load_state header");
+    e = hipMemcpyAsync(h->ws, (const unsigned char *)src + hdr.size(), h->total, hipMemcpyDeviceToDevice, s);
+    if (e) return hip_fail(h, e, "load_state copy");
+    // the host mirrors only once the workspace copy is queued: a failed copy leaves them as they were
     std::memcpy(h->game_map.data(), hdr.data() + sizeof sh, (size_t)h->ngames * sizeof(int32_t));
     std::memcpy(h->parked.data(), hdr.data() + sizeof sh + (size_t)h->ngames * sizeof(int32_t), (size_t)h->ngames);
     h->bots_ready = sh.bots_ready != 0;
-    e = hipMemcpyAsync(h->ws, (const unsigned char *)src + hdr.size(), h->total, hipMemcpyDeviceToDevice, s);
-    if (e) return hip_fail(h, e, "load_state copy");
     h->base.parked = sh.parked_any ? (uint8_t *)(h->ws + h->off_parked) : nullptr;
     EngineParams p = h->base;
     p.obs = obs;

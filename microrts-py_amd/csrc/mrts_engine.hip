@@ -357,7 +357,6 @@ __device__ __forceinline__ void store_game(const EngineParams& p, const Lds& L, 
     if (threadIdx.x < MRTS_GENV_WORDS) p.genv[(size_t)g * MRTS_GENV_WORDS + threadIdx.x] = L.sc[threadIdx.x];
 }
 
-// write the one-hot observation of one view: bits in L.aux, 16-byte stores
 // PartiallyObservableGameState.observable for both players: a cell is seen by
 // player q when some unit of q is within its sight radius (d^2 <= r^2).  Each
 // unit lane ORs its sight disk into the player's LDS bitmap, one row span per
@@ -376,21 +375,8 @@ __device__ __forceinline__ void compute_vis(const EngineParams& p, const Lds& L)
     __syncthreads();
 }
 
-// All outputs of one game once its state is final.  Phase A (lane per cell):
-// every view's one-hot word and, with `masks`, its getMasks(0) 79-bit word
-// (+ the source channel, written straight out) into LDS; one barrier; phase B:
-// the views' obs rows, then their mask rows, streamed with 16-byte stores and no
-// further barrier (the envs of a game are adjacent: a selfplay pair 2k, 2k+1
-// writes one contiguous run).  The words live in the region of the step's
-// scratch lists (resv .. snap), dead by now.
-// `skip`: lanes [0, skip) leave after phase A (the bot-fused k_step's wave 0) and
-// the others stream phase B alone.
-// `early_cnt` (the early-bot k_step): wave 0 is running the bot already, so
-// phase A too runs on lanes [skip, NT) only and its end is a counter the
-// streaming waves meet at in LDS instead of a workgroup barrier.
-// res0 / res1: the players' resources (the masks' produce checks), read by the
-// caller from L.sc before the early bot may overwrite the step's scalars.
-template <int NT, int P, typename OT>
+// phase A's one-hot word of cell c for every view of the game (into L.outw)
+template <int P>
 __device__ __forceinline__ void onehot_words(const EngineParams& p, const Lds& L, const Game& G, int c) {
     const int HW = p.HW, nw = HW / 32 + 1;
     const uint32_t u = L.unit[c], a = L.act[c];
@@ -539,7 +525,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
             }
             __syncthreads();
         }
-        for (int c = threadIdx.x; c < HW; c += NT) onehot_words<NT, P, OT>(p, L, G, c);
+        for (int c = threadIdx.x; c < HW; c += NT) onehot_words<P>(p, L, G, c);
         __syncthreads();
         stream_obs<P, OT>(p, L, G, threadIdx.x, NT);
         MRTS_STAMP_MAX(9, (threadIdx.x & 63) == 0);
@@ -548,7 +534,7 @@ __device__ __forceinline__ void emit_outputs(const EngineParams& p, const Lds& L
     if (obs && P == 31) compute_vis<NT>(p, L);
     const int a0 = early_cnt ? skip : 0;   // phase A's first lane
     for (int c = (int)threadIdx.x - a0; c < HW; c += NT - a0) {
-        if (obs) onehot_words<NT, P, OT>(p, L, G, c);
+        if (obs) onehot_words<P>(p, L, G, c);
         if (masks) mask_words(p, L, G, c, res0, res1);
     }
     if (early_cnt) {   // the streaming waves' own meeting point (wave 0 never arrives)

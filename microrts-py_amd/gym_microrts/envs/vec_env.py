@@ -697,7 +697,9 @@ class MapCycle:
 def _set_states_atomic(envs, states):
     """set_state on several engines as one operation: every snapshot is checked first, and if
     an engine still refuses its snapshot (mrts_load_state's configuration fingerprint), the
-    engines restored before it are rolled back to where they were."""
+    engines restored before it -- and the refusing engine itself, which mrts_load_state may
+    have left half-restored if it failed after its header checks -- are rolled back to
+    where they were."""
     for e, st in zip(envs, states):
         e._check_state(st)
     before = [e.get_state() for e in envs]
@@ -706,7 +708,7 @@ def _set_states_atomic(envs, states):
         for e, st in zip(envs, states):
             out.append(e.set_state(st))
     except Exception:
-        for e, st in zip(envs[:len(out)], before):
+        for e, st in zip(envs[:len(out) + 1], before):
             e.set_state(st)
         raise
     return out

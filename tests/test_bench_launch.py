@@ -145,8 +145,20 @@ def test_dist_backend_defaults_to_gloo():
     """The timing barrier / max-over-ranks / per-rank gather run on gloo unless asked:
     no data-path collective exists, so RCCL is not needed for the curve."""
     a = bench.parse(["--gpus", "8"])
-    assert a.dist_backend == "gloo" and a.rank_timeout == 900.0
+    assert a.dist_backend == "gloo"
     assert bench.parse(["--dist-backend", "nccl"]).dist_backend == "nccl"
+
+
+def test_rank_timeout_default_scales_with_the_requested_work():
+    """the default deadline grows with steps / warm-up / pre-roll / seeds, so a
+    legitimately long scale run is not killed at a fixed 15 minutes; an explicit value wins."""
+    a = bench.parse(["--gpus", "8"])   # 2000 pre-roll + 50 warm-up + 300 steps
+    assert a.rank_timeout == 900.0 + 0.05 * 2350
+    long = bench.parse(["--gpus", "8", "--steps", "100000", "--seeds", "3"])
+    assert long.rank_timeout == 900.0 + 0.05 * 3 * (2000 + 50 + 100000)
+    assert long.rank_timeout > 60 * 60 * 4   # > 100x the ~0.25 ms a tick takes
+    assert bench.parse(["--rank-timeout", "0"]).rank_timeout == 0
+    assert bench.parse(["--rank-timeout", "42"]).rank_timeout == 42
 
 
 def test_per_rank_single():

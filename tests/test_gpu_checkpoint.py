@@ -14,7 +14,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits bel
 W = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
 
 
-def _env(partial_obs=False, bot_fusion=True, cycle=False, n=32, bots=None, map_path="maps/16x16/basesWorkers16x16.xml"):
+def _env(partial_obs=False, bot_fusion=True, cycle=False, n=32, bots=None, map_path="maps/16x16/basesWorkers16x16.xml",
+         max_steps=60):
     import torch
 
     from gym_microrts import microrts_ai
@@ -22,7 +23,7 @@ def _env(partial_obs=False, bot_fusion=True, cycle=False, n=32, bots=None, map_p
 
     bots = bots or [microrts_ai.coacAI, microrts_ai.workerRushAI, microrts_ai.randomBiasedAI, microrts_ai.lightRushAI] * (n // 8)
     kw = dict(cycle_maps=["maps/16x16/basesWorkers16x16.xml", "maps/16x16/basesWorkers16x16A.xml"]) if cycle else {}
-    return MicroRTSGridModeVecEnv(num_selfplay_envs=n // 2, num_bot_envs=len(bots), max_steps=60, ai2s=bots,
+    return MicroRTSGridModeVecEnv(num_selfplay_envs=n // 2, num_bot_envs=len(bots), max_steps=max_steps, ai2s=bots,
                                   map_paths=[map_path], partial_obs=partial_obs, reward_weight=W,
                                   return_tensors=True, obs_dtype=torch.int32, bot_fusion=bot_fusion, **kw)
 
@@ -88,11 +89,12 @@ def test_checkpoint_of_another_config_refused():
     other.close()
 
 
-@pytest.mark.parametrize("what", ["bots", "map", "partial_obs"])
+@pytest.mark.parametrize("what", ["bots", "map", "partial_obs", "max_steps"])
 def test_checkpoint_same_shape_other_config_refused(what):
     """a snapshot of a handle with the same shape (games, cells, map count,
     workspace size) but other bots, another map or another obs layout would copy that
-    handle's device tables in; the header's configuration fingerprint refuses it."""
+    handle's device tables in; the header's configuration fingerprint refuses it.
+    ADVICE r5: another time limit too (the continuation would differ from the saved run)."""
     from gym_microrts import _native, microrts_ai
 
     env = _env(n=32)
@@ -100,6 +102,8 @@ def test_checkpoint_same_shape_other_config_refused(what):
         other = _env(n=32, bots=[microrts_ai.workerRushAI] * 16)
     elif what == "map":
         other = _env(n=32, map_path="maps/16x16/basesWorkers16x16B.xml")   # (16x16A is byte-identical to 16x16)
+    elif what == "max_steps":
+        other = _env(n=32, max_steps=61)
     else:
         other = _env(n=32, partial_obs=True)
     env.reset()

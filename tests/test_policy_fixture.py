@@ -41,3 +41,50 @@ def test_policy_acts_within_masks_on_the_oracle():
             assert (valid[has_any] == 1).all(), f"component {k} picked an invalid entry at tick {s}"
         obs, _, _, _ = o.step(a)
     o.close()
+
+
+def _full_reference_state_dict():
+    """A synthetic full ppo_gridnet Agent state_dict (experiments/ppo_gridnet.py:191-212
+    names: encoder.{1,4}, actor.{0,2} and critic.{1,3}) -- 12 tensors, as agent_sota.pt holds."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "examples"))
+    from ppo_gridnet_driver import GridNet
+
+    src = GridNet(29, 16, 16).state_dict()
+    inv = {v: k for k, v in GridNet.REFERENCE_NAMES.items()}
+    out = {}
+    for name, t in src.items():
+        layer, _, field = name.rpartition(".")
+        out[f"{inv[layer]}.{field}"] = t.clone() + 0.25
+    assert len(out) == 12 and "critic.3.bias" in out
+    return GridNet, out
+
+
+def test_full_agent_state_dict_loads_with_critic(tmp_path):
+    """a full reference state_dict (critic included) is the documented
+    --agent-model-path input; load_reference_policy takes all 12 tensors, through
+    load_weights' torch.load(weights_only=True) path."""
+    GridNet, sd = _full_reference_state_dict()
+    from ppo_gridnet_driver import load_weights
+
+    p = tmp_path / "agent_full.pt"
+    torch.save(sd, p)
+    net = GridNet(29, 16, 16)
+    done = net.load_reference_policy(load_weights(str(p)))
+    assert sorted(done) == sorted(sd)
+    assert torch.equal(net.state_dict()["v.3.bias"], sd["critic.3.bias"])
+    assert torch.equal(net.state_dict()["pi.2.weight"], sd["actor.2.weight"])
+
+
+def test_policy_state_dict_missing_actor_raises():
+    import pytest
+
+    GridNet, sd = _full_reference_state_dict()
+    del sd["actor.2.bias"]
+    with pytest.raises(ValueError, match="actor.2.bias"):
+        GridNet(29, 16, 16).load_reference_policy(sd)
+    _, sd = _full_reference_state_dict()
+    sd["encoder.1.weight"] = sd["encoder.1.weight"][:, :5]
+    with pytest.raises(ValueError, match="encoder.1.weight"):
+        GridNet(29, 16, 16).load_reference_policy(sd)
