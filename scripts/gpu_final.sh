@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p "$O"
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 \
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread --durations=40 > "$O/pytest_gpu.log" 2>&1 \
   || { echo "pytest failed"; tail -40 "$O/pytest_gpu.log"; exit 1; }
 tail -1 "$O/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "smoke failed"; tail -20 "$O/smoke.log"; exit 1; }

@@ -14,7 +14,7 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fu
   -k "float32 or obs_dtype or fullsize" --timeout 600 --timeout-method thread --durations=0 > "$O/pytest_float.log" 2>&1 \
   || { echo "pytest failed"; tail -40 "$O/pytest_float.log"; exit 1; }
 tail -1 "$O/pytest_float.log"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o headline -- python -u -m pytest \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o headline -- python -u -m pytest \
   "tests/test_gpu_fullsize.py::test_fullsize_headline_8192_staggered_2000_ticks[float32]" -x -q --timeout 350 \
   --timeout-method thread > "$O/rocprof_headline.log" 2>&1 || { echo "rocprof run failed"; tail -30 "$O/rocprof_headline.log"; exit 1; }
 tail -1 "$O/rocprof_headline.log"
