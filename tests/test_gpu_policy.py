@@ -11,8 +11,8 @@ are sampled once per tick on the GPU from the engine's own obs and masks
 array is fed to the HIP engine and to the oracle, so floating point never enters the
 comparison.  basesWorkers16x16A (the eval script's map), 256 selfplay envs + 256
 envs vs device coacAI / workerRushAI, 1100 ticks, max_steps 800 (time-limit resets
-inside the window): obs, masks, source mask, raw rewards and dones bit-equal every
-tick.  The trajectories' statistics (the oracle's event counters) are recorded and
+inside the window): obs (float32, as ppo_gridnet.py consumes them, compared as
+bits), masks, source mask, raw rewards and dones bit-equal every tick.  The trajectories' statistics (the oracle's event counters) are recorded and
 must lie clearly above the random sampler's on the same envs and ticks."""
 import json
 import os
@@ -20,7 +20,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import MAPS
+from conftest import MAPS, obs_bits_equal
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -56,7 +56,7 @@ def test_trained_policy_lockstep_matches_oracle():
     ais = ["coacAI", "workerRushAI"] * (nbot // 2)
     g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=max_steps, map_paths=[MAP],
                                ai2s=[getattr(microrts_ai, a) for a in ais], reward_weight=W, return_tensors=True,
-                               obs_dtype=torch.int32)
+                               obs_dtype=torch.float32)
     o = OracleVecEnv(nsp, nbot, [os.path.join(MAPS, MAP)], max_steps=max_steps, ai2s=ais, reward_weight=W)
     dev = g.device
     net = load_policy(dev)
@@ -67,7 +67,7 @@ def test_trained_policy_lockstep_matches_oracle():
         assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"{what} differs at tick {s}"
 
     obs = g.reset()
-    same(obs, o.reset(), "reset obs", -1)
+    assert obs_bits_equal(obs, o.reset()), "reset obs"
     raw_sum, wins = np.zeros(6), 0
     for s in range(ticks):
         mg, mo = g.get_action_mask(), o.get_action_mask()
@@ -77,7 +77,7 @@ def test_trained_policy_lockstep_matches_oracle():
         obs, rg, dg, ig = g.step(a)
         oo, ro, do, io = o.step(a.cpu().numpy())
         raw = np.array([i["raw_rewards"] for i in io])
-        same(obs, oo, "obs", s)
+        assert obs_bits_equal(obs, oo), f"obs differs at tick {s}"   # float32: ppo_gridnet's dtype
         same(ig._raw, raw, "raw rewards", s)
         same(dg, np.asarray(do, bool), "done", s)
         raw_sum += raw[p0].sum(0)
@@ -135,7 +135,7 @@ def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps, parti
     ais = (bots * n)[:n]
     g = MicroRTSGridModeVecEnv(num_selfplay_envs=n, num_bot_envs=n, max_steps=max_steps, map_paths=[map_path],
                                ai2s=[getattr(microrts_ai, a) for a in ais], reward_weight=W, return_tensors=True,
-                               obs_dtype=torch.int32, partial_obs=partial_obs)
+                               obs_dtype=torch.float32, partial_obs=partial_obs)
     o = OracleVecEnv(n, n, [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais, reward_weight=W,
                      partial_obs=partial_obs)
     dev = g.device
@@ -146,7 +146,7 @@ def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps, parti
         assert torch.equal(gpu, torch.from_numpy(np.ascontiguousarray(host)).to(dev)), f"{what} differs at tick {s}"
 
     obs = g.reset()
-    same(obs, o.reset(), "reset obs", -1)
+    assert obs_bits_equal(obs, o.reset()), "reset obs"
     wins = 0
     for s in range(ticks):
         mg, mo = g.get_action_mask(), o.get_action_mask()
@@ -155,7 +155,7 @@ def test_trained_policy_lockstep_other_maps(map_path, n, ticks, max_steps, parti
         obs, _, dg, ig = g.step(a)
         oo, ro, do, io = o.step(a.cpu().numpy())
         raw = np.array([i["raw_rewards"] for i in io])
-        same(obs, oo, "obs", s)
+        assert obs_bits_equal(obs, oo), f"obs differs at tick {s}"   # float32: ppo_gridnet's dtype
         same(ig._raw, raw, "raw rewards", s)
         same(dg, np.asarray(do, bool), "done", s)
         wins += int((raw[_p0_envs(n, n), 0] > 0).sum())
