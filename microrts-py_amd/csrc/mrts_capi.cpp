@@ -230,7 +230,8 @@ int mrts_create(const mrts_config *cfg, mrts_vec **out) {
     h->H = h->maps[0].h;
     h->HW = h->W * h->H;
     if (mrts_engine_lds_bytes(h->HW, h->W) > 65536)
-        return fail(h, MRTS_ENOTIMPL, "map too large for one workgroup's LDS (max 24x24-class maps so far)");
+        return fail(h, MRTS_ENOTIMPL, "map too large: the step kernel's workgroup LDS carve exceeds 64 KB (maps up to "
+                                      "about 1128 cells fit, e.g. 32x32, 33x33, 47x24; DESIGN.md §3)");
     h->game_map.assign(h->ngames, 0);
     for (int g = 0; g < h->ngames; g++) {
         int m = cfg->game_map ? cfg->game_map[g] : 0;

@@ -538,3 +538,74 @@ def test_grouped_source_sampler_empty_segment():
     _native.check(lib.mrts_sample_actions_src_group(st, (_native.SampleSeg * 3)(*segs), 3, ctypes.c_uint64(3), 4))
     for out, ref in zip(outs, refs):
         assert torch.equal(out, ref)   # the empty segment's buffer untouched (-1 both)
+
+
+@pytest.mark.parametrize("return_tensors", [False, True])
+def test_reward_shaping_off(return_tensors):
+    """reward_shaping=False (vec_env.py:1004-1005): every raw reward channel but WinLoss reads
+    0 -- in infos, in `raw @ reward_weight` and in the tensor path's fused dot -- while the
+    game itself runs as with shaping (obs, masks, dones == the oracle's)."""
+    from oracle_py import sample_actions
+
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from oracle_py import OracleVecEnv
+
+    torch = _torch()
+    m, w = "maps/8x8/basesWorkers8x8.xml", np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=16, num_bot_envs=8, max_steps=300, map_paths=[m], reward_weight=w,
+                               ai2s=[microrts_ai.workerRushAI] * 8, reward_shaping=False, return_tensors=return_tensors,
+                               obs_dtype=torch.int32 if return_tensors else None)
+    o = OracleVecEnv(16, 8, [os.path.join(MAPS, m)], max_steps=300, ai2s=["workerRushAI"] * 8, reward_weight=w)
+    cpu = (lambda t: t.cpu().numpy()) if return_tensors else np.asarray
+    np.testing.assert_array_equal(cpu(g.reset()), o.reset())
+    seen_win = seen_shaped = 0
+    for s in range(700):
+        mo = o.get_action_mask()
+        np.testing.assert_array_equal(cpu(g.get_action_mask()), mo, err_msg=f"mask {s}")
+        a = sample_actions(mo, 13, s)
+        og, rg, dg, ig = g.step(torch.from_numpy(a).to(g.device) if return_tensors else a)
+        oo, ro, do, io = o.step(a)
+        raw_o = np.array([i["raw_rewards"] for i in io])
+        seen_shaped += int((raw_o[:, 1:] != 0).any())
+        raw_o[:, 1:] = 0
+        seen_win += int((raw_o[:, 0] != 0).any())
+        np.testing.assert_array_equal(cpu(og), oo, err_msg=f"obs {s}")
+        np.testing.assert_array_equal(np.array([np.asarray(i["raw_rewards"]) for i in ig]), raw_o, err_msg=f"raw {s}")
+        np.testing.assert_allclose(cpu(rg), raw_o @ g.reward_weight, rtol=0, atol=1e-12, err_msg=f"reward {s}")
+        np.testing.assert_array_equal(cpu(dg), do)
+    assert seen_shaped > 0 and seen_win > 0   # shaped channels were zeroed; WinLoss got through
+    assert g.error_flags() == 0
+
+
+def test_per_env_map_paths():
+    """map_paths with one entry per env (vec_env.py:120-125; all of one size): every game
+    starts on its own env's map -- a selfplay pair on its first env's -- and auto-resets
+    onto it again.  GPU == an oracle given the same per-game map table."""
+    from gym_microrts import microrts_ai
+    from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
+    from gym_microrts.microrts_maps import ALL16x16_MAPS
+    from oracle_py import OracleVecEnv, sample_actions
+
+    nsp, nbot = 12, 6
+    paths = [ALL16x16_MAPS[(3 * e) % len(ALL16x16_MAPS)] for e in range(nsp + nbot)]
+    w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
+    bots = ["coacAI", "workerRushAI", "lightRushAI"] * 2
+    g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=nbot, max_steps=80, map_paths=paths, reward_weight=w,
+                               ai2s=[getattr(microrts_ai, b) for b in bots])
+    table = list(dict.fromkeys(paths))
+    game_env = [2 * k for k in range(nsp // 2)] + [nsp + j for j in range(nbot)]
+    o = OracleVecEnv(nsp, nbot, [os.path.join(MAPS, p) for p in table], max_steps=80, ai2s=bots, reward_weight=w,
+                     game_maps=[table.index(paths[e]) for e in game_env])
+    assert len(set(paths[e] for e in game_env)) > 5
+    np.testing.assert_array_equal(g.reset(), o.reset())
+    for s in range(250):
+        mo = o.get_action_mask()
+        np.testing.assert_array_equal(g.get_action_mask(), mo, err_msg=f"mask {s}")
+        a = sample_actions(mo, 17, s)
+        og, rg, dg, _ = g.step(a)
+        oo, ro, do, _ = o.step(a)
+        np.testing.assert_array_equal(og, oo, err_msg=f"obs {s}")
+        np.testing.assert_array_equal(rg, ro, err_msg=f"reward {s}")
+        np.testing.assert_array_equal(dg, do)
+    assert g.error_flags() == 0
