@@ -22,6 +22,12 @@ The generator's own variation, all kept as it writes it:
   generator's).
 
     python tests/golden/make_pcg_maps.py
+
+A campaign set, `--campaign N` (tests/golden/maps/pcg_campaign.json): N more maps from the
+same generator, each with its own seed, its size drawn from 8..24 (a quarter of them
+non-square) and one or two bases per side, the generator drawing wallRings and the
+obstacles itself -- the XML text of each is stored in the JSON (data, as the generator
+wrote it) for tests/test_pcg_maps.py's campaign lock-step.
 """
 import contextlib
 import hashlib
@@ -107,8 +113,38 @@ def generate(pcg, w, h, rings, bases, seed0):
     raise RuntimeError(f"no seed for {w}x{h} rings={rings}")
 
 
+def campaign(pcg, n, out):
+    import numpy as np
+
+    rng = np.random.default_rng(20261018)
+    maps = []
+    for k in range(n):
+        w = int(rng.integers(8, 25))
+        h = w if rng.random() < 0.75 else int(rng.integers(8, 25))
+        bases = 1 if rng.random() < 0.7 else 2
+        seed0 = 100_000 + 1000 * k
+        for seed in range(seed0, seed0 + 1000):   # any wallRings: the generator's own draw
+            random.seed(seed)
+            rings = pcg.PCG(width=w, height=h, unit_location_records=[], base_location_records=[]).wallRings
+            try:
+                got, data = generate(pcg, w, h, rings, bases, seed)
+            except RuntimeError:
+                continue
+            if got == seed:
+                break
+        maps.append({"seed": got, "width": w, "height": h, "wallRings": rings, "bases_per_side": bases,
+                     "xml": data.decode()})
+    with open(out, "w") as f:
+        json.dump({"generator": REF_PCG, "generator_sha256": hashlib.sha256(open(REF_PCG, "rb").read()).hexdigest(),
+                   "maps": maps}, f)
+        f.write("\n")
+    print("wrote", out, len(maps), "maps")
+
+
 def main():
     pcg = load_pcg()
+    if len(sys.argv) == 3 and sys.argv[1] == "--campaign":
+        return campaign(pcg, int(sys.argv[2]), os.path.join(os.path.dirname(OUT), "pcg_campaign.json"))
     src_sha = hashlib.sha256(open(REF_PCG, "rb").read()).hexdigest()
     os.makedirs(OUT, exist_ok=True)
     manifest = {"generator": "/root/reference/PCG/pcg.py", "generator_sha256": src_sha, "maps": []}

@@ -105,3 +105,37 @@ def test_fuzz_bot_vs_bot_lockstep(tmp_path, seed):
     assert g.error_flags() == 0
     g.close()
     o.close()
+
+
+def large_case(seed):
+    """A random shape past 32x32 that mrts_create still accepts (1025..1128 cells: the step's
+    unprefetched path, tests/test_max_map_sizes.py), bots only where they are allowed (at
+    most 32 wide and 64 high)."""
+    import ctypes
+
+    from gym_microrts import _native
+
+    f = _native.lib().mrts_engine_lds_bytes
+    f.restype, f.argtypes = ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(7000 + seed)
+    while True:
+        w, h = int(rng.integers(12, 72)), int(rng.integers(12, 72))
+        if 1024 < w * h <= 1200 and f(w * h, w) <= 65536:
+            break
+    bots_ok = w <= 32 and h <= 64
+    bots = [str(b) for b in rng.choice(BOTS + ["passiveAI"], size=int(rng.integers(0, 6)))] if bots_ok else []
+    return dict(w=w, h=h, n=int(rng.integers(20, 260)), walls=float(rng.uniform(0, 0.2)),
+                res=(int(rng.integers(0, 30)), int(rng.integers(0, 30))), bots=bots,
+                nsp=2 * int(rng.integers(0 if bots else 1, 3)), partial=bool(rng.integers(0, 2)),
+                max_steps=int(rng.integers(30, 150)))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", range(FIRST, FIRST + max(1, SEEDS // 6)))
+def test_fuzz_large_map_lockstep(tmp_path, seed):
+    """Random maps of the largest accepted shapes (past 1024 cells), random bots where allowed,
+    fog, time limits, masked and unmasked actions: GPU == oracle every tick."""
+    c = large_case(seed)
+    path = write_random_map(str(tmp_path / f"L{seed}.xml"), c["w"], c["h"], seed, n_units=c["n"], wall_frac=c["walls"],
+                            res=c["res"])
+    lockstep(c["bots"], path, c["nsp"], 120, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed")

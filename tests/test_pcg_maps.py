@@ -95,3 +95,45 @@ def test_gpu_lockstep_pcg_map(name, partial_obs):
 
     out = lockstep(["coacAI", "workerRushAI"] * 2, _path(name), 4, 400, partial_obs=partial_obs, seed=31, max_steps=150)
     assert out.sum() >= 8   # every game ended (gameover or time limit) at least once
+
+
+# ---- campaign: 300 more generator maps (tests/golden/make_pcg_maps.py --campaign 300) ----
+CAMPAIGN = json.load(open(os.path.join(REPO, "tests", "golden", "maps", "pcg_campaign.json")))
+NCAMP = int(os.environ.get("MRTS_PCG_CAMPAIGN", "8"))   # GPU cases by default (the full set: 300)
+
+
+def _campaign_map(tmp_path, k):
+    m = CAMPAIGN["maps"][k]
+    p = tmp_path / f"pcg_campaign_{k}.xml"
+    p.write_text(m["xml"])
+    return str(p), m
+
+
+def test_campaign_maps_load_in_both_loaders(tmp_path):
+    from gym_microrts import _native
+    from oracle_py import parse_map
+
+    assert len(CAMPAIGN["maps"]) == 300 and CAMPAIGN["generator_sha256"] == MANIFEST["generator_sha256"]
+    shapes = set()
+    for k in range(len(CAMPAIGN["maps"])):
+        p, m = _campaign_map(tmp_path, k)
+        pm = parse_map(p)
+        assert (pm["width"], pm["height"]) == (m["width"], m["height"])
+        assert len(pm["units"]) == 4 + 2 * m["bases_per_side"] + 2
+        hd = _native.create(2, 2, 100, False, [p], [0, 0, 0], [0, 4], 1)
+        _native.lib().mrts_destroy(hd)
+        shapes.add((m["width"], m["height"], m["wallRings"], m["bases_per_side"]))
+    assert len(shapes) > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("k", range(NCAMP))
+def test_gpu_lockstep_pcg_campaign(tmp_path, k):
+    """Campaign map k: 4 selfplay envs + coacAI / workerRushAI / lightRushAI / randomBiasedAI,
+    300 ticks, max_steps 120, fog on odd k: HIP == oracle every tick."""
+    from test_gpu_bots import lockstep
+
+    p, m = _campaign_map(tmp_path, k)
+    lockstep(["coacAI", "workerRushAI", "lightRushAI", "randomBiasedAI"], p, 4, 300, partial_obs=bool(k % 2), seed=k,
+             max_steps=120)
