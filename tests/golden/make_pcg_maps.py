@@ -122,7 +122,7 @@ def campaign(pcg, n, out):
         w = int(rng.integers(8, 25))
         h = w if rng.random() < 0.75 else int(rng.integers(8, 25))
         bases = 1 if rng.random() < 0.7 else 2
-        seed0 = 100_000 + 1000 * k
+        seed0, got = 100_000 + 1000 * k, None
         for seed in range(seed0, seed0 + 1000):   # any wallRings: the generator's own draw
             random.seed(seed)
             rings = pcg.PCG(width=w, height=h, unit_location_records=[], base_location_records=[]).wallRings
@@ -132,6 +132,8 @@ def campaign(pcg, n, out):
                 continue
             if got == seed:
                 break
+        if got is None:
+            raise RuntimeError(f"campaign map {k}: no seed in [{seed0}, {seed0 + 1000}) generated a {w}x{h} map")
         maps.append({"seed": got, "width": w, "height": h, "wallRings": rings, "bases_per_side": bases,
                      "xml": data.decode()})
     with open(out, "w") as f:
