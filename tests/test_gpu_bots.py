@@ -16,8 +16,12 @@ BOTS = ["workerRushAI", "lightRushAI", "coacAI", "randomBiasedAI", "randomAI", "
 
 
 def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=2000, mode="masked", return_tensors=False,
-             bot_fusion=True):
+             bot_fusion=True, obs_dtype="int32"):
+    """obs_dtype (tensor path only): "int32", or "float32" -- the bench's dtype, compared as
+    bits against the oracle's one-hot (conftest.obs_bits_equal)."""
     import torch
+
+    from conftest import obs_bits_equal
 
     from gym_microrts import microrts_ai
     from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
@@ -27,11 +31,18 @@ def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=200
     g = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=len(ais), max_steps=max_steps,
                                ai2s=[getattr(microrts_ai, a) for a in ais], map_paths=[map_path], reward_weight=w,
                                partial_obs=partial_obs, return_tensors=return_tensors,
-                               obs_dtype=torch.int32 if return_tensors else None, bot_fusion=bot_fusion)
+                               obs_dtype=getattr(torch, obs_dtype) if return_tensors else None, bot_fusion=bot_fusion)
     o = OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, map_path)], max_steps=max_steps, ai2s=ais,
                      partial_obs=partial_obs, reward_weight=w)
     cpu = (lambda t: t.cpu().numpy()) if return_tensors else np.asarray
-    np.testing.assert_array_equal(cpu(g.reset()), o.reset())
+
+    def check_obs(got, want, msg):
+        if return_tensors and obs_dtype == "float32":
+            assert obs_bits_equal(got, want), msg
+        else:
+            np.testing.assert_array_equal(cpu(got), want, err_msg=msg)
+
+    check_obs(g.reset(), o.reset(), "reset")
     rng = np.random.default_rng(seed)
     n, hw = g.num_envs, g.height * g.width
     nvec = np.array([6, 4, 4, 4, 4, 7, 49])
@@ -46,7 +57,7 @@ def lockstep(ais, map_path, nsp, steps, partial_obs=False, seed=7, max_steps=200
         ga = torch.from_numpy(a).to(g.device) if return_tensors else a
         og, rg, dg, ig = g.step(ga)
         oo, ro, do, io = o.step(a)
-        np.testing.assert_array_equal(cpu(og), oo, err_msg=f"obs step {s}")
+        check_obs(og, oo, f"obs step {s}")
         raw_g = np.array([i["raw_rewards"] for i in ig])
         raw_o = np.array([i["raw_rewards"] for i in io])
         np.testing.assert_array_equal(raw_g, raw_o, err_msg=f"raw rewards step {s}")
@@ -166,10 +177,12 @@ def test_league_outcomes_on_device():
     assert g.error_flags() == 0
 
 
-def mixed_lockstep(spec, steps, max_steps=300, partial_obs=False, **kw):
+def mixed_lockstep(spec, steps, max_steps=300, partial_obs=False, obs_dtype="int32", **kw):
     """MicroRTSMixedMapVecEnv (kw: concurrent / group_policy) vs one oracle per bucket:
-    obs, masks, rewards and dones bit-exact every step."""
+    obs (int32, or float32 compared as bits), masks, rewards and dones bit-exact every step."""
     import torch
+
+    from conftest import obs_bits_equal
 
     from gym_microrts import microrts_ai
     from gym_microrts.envs.vec_env import MicroRTSMixedMapVecEnv
@@ -178,11 +191,11 @@ def mixed_lockstep(spec, steps, max_steps=300, partial_obs=False, **kw):
     w = np.array([10.0, 1.0, 1.0, 0.2, 1.0, 4.0])
     env = MicroRTSMixedMapVecEnv([dict(map_paths=[m], num_selfplay_envs=nsp, ai2s=[getattr(microrts_ai, a) for a in ais])
                                   for m, nsp, ais in spec], max_steps=max_steps, return_tensors=True, partial_obs=partial_obs,
-                                 reward_weight=w, obs_dtype=torch.int32, **kw)
+                                 reward_weight=w, obs_dtype=getattr(torch, obs_dtype), **kw)
     orc = [OracleVecEnv(nsp, len(ais), [os.path.join(MAPS, m)], max_steps=max_steps, ai2s=ais, reward_weight=w,
                         partial_obs=partial_obs) for m, nsp, ais in spec]
     for og, oo in zip(env.reset(), [o.reset() for o in orc]):
-        np.testing.assert_array_equal(og.cpu().numpy(), oo)
+        assert obs_bits_equal(og, oo), "reset"
     for s in range(steps):
         masks = env.get_action_mask()
         acts = []
@@ -193,7 +206,7 @@ def mixed_lockstep(spec, steps, max_steps=300, partial_obs=False, **kw):
         obs, rew, done, infos = env.step([torch.from_numpy(a).cuda() for a in acts])
         for k, o in enumerate(orc):
             oo, ro, do, _ = o.step(acts[k])
-            np.testing.assert_array_equal(obs[k].cpu().numpy(), oo, err_msg=f"bucket {k} step {s}")
+            assert obs_bits_equal(obs[k], oo), f"obs bucket {k} step {s}"
             np.testing.assert_array_equal(rew[k].cpu().numpy(), ro, err_msg=f"bucket {k} step {s}")
             np.testing.assert_array_equal(done[k].cpu().numpy(), do)
     assert env.error_flags() == 0

@@ -3,7 +3,9 @@ density 0-25 %, 4 to 200 units of every type, random starting resources, a rando
 device bots, selfplay pairs, full or partial observability, random time limits, masked and
 unmasked agent actions.  MRTS_FUZZ_SEEDS / MRTS_FUZZ_FIRST set the number of cases and the
 first seed (default 12 from 0; the round-5 campaign ran seeds 0-2199 of the single-engine
-cases and 0-1499 of the grouped-launch cases, profiles/r05_fuzz/)."""
+cases and 0-1499 of the grouped-launch cases, profiles/r05_fuzz/).  Odd seeds run the tensor
+path with float32 obs -- the bench's kernels -- compared as bits (conftest.obs_bits_equal);
+even seeds the int32 numpy / tensor contracts."""
 import os
 
 import numpy as np
@@ -15,6 +17,11 @@ from test_gpu_bots import BOTS, lockstep
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]   # per-test limits below override
 SEEDS = int(os.environ.get("MRTS_FUZZ_SEEDS", "12"))
 FIRST = int(os.environ.get("MRTS_FUZZ_FIRST", "0"))
+
+
+def f32(seed):
+    """odd seeds: the tensor path with float32 obs (the bench's dtype), compared as bits"""
+    return dict(return_tensors=True, obs_dtype="float32") if seed % 2 else {}
 
 
 def case(seed):
@@ -33,7 +40,8 @@ def test_fuzz_map_lockstep(tmp_path, seed):
     c = case(seed)
     path = write_random_map(str(tmp_path / f"fuzz{seed}.xml"), c["w"], c["h"], seed, n_units=min(c["n"], c["w"] * c["h"] - 4),
                             wall_frac=c["walls"], res=c["res"])
-    lockstep(c["bots"], path, c["nsp"], 160, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed")
+    lockstep(c["bots"], path, c["nsp"], 160, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed",
+             **f32(seed))
 
 
 def group_case(seed):
@@ -64,7 +72,8 @@ def test_fuzz_step_group_lockstep(tmp_path, seed):
         path = write_random_map(str(tmp_path / f"g{seed}_{k}.xml"), c["w"], c["h"], seed * 10 + k,
                                 n_units=min(c["n"], c["w"] * c["h"] - 4), wall_frac=c["walls"])
         rows.append((path, c["nsp"], c["bots"]))
-    env = mixed_lockstep(rows, 120, max_steps=max_steps, partial_obs=partial, group_policy=policy)
+    env = mixed_lockstep(rows, 120, max_steps=max_steps, partial_obs=partial, group_policy=policy,
+                         obs_dtype=f32(seed).get("obs_dtype", "int32"))
     assert env.grouped
 
 
@@ -138,4 +147,5 @@ def test_fuzz_large_map_lockstep(tmp_path, seed):
     c = large_case(seed)
     path = write_random_map(str(tmp_path / f"L{seed}.xml"), c["w"], c["h"], seed, n_units=c["n"], wall_frac=c["walls"],
                             res=c["res"])
-    lockstep(c["bots"], path, c["nsp"], 120, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed")
+    lockstep(c["bots"], path, c["nsp"], 120, partial_obs=c["partial"], seed=seed, max_steps=c["max_steps"], mode="mixed",
+             **f32(seed))

@@ -21,4 +21,5 @@ BOTS = ["coacAI", "workerRushAI", "lightRushAI", "randomBiasedAI", "POWorkerRush
                                               (16, 16, 60, 5)])
 def test_random_map_lockstep(tmp_path, w, h, n_units, seed, partial_obs):
     path = write_random_map(str(tmp_path / f"r{w}x{h}_{seed}.xml"), w, h, seed, n_units=n_units)
-    lockstep(BOTS * 2, path, 4, 300, partial_obs=partial_obs, seed=seed, max_steps=200, mode="mixed")
+    f32 = dict(return_tensors=True, obs_dtype="float32") if seed % 2 else {}   # odd seeds: the bench's dtype, as bits
+    lockstep(BOTS * 2, path, 4, 300, partial_obs=partial_obs, seed=seed, max_steps=200, mode="mixed", **f32)

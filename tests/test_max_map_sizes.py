@@ -69,14 +69,16 @@ def test_oracle_runs_the_boundary_shapes(tmp_path):
 @pytest.mark.parametrize("w,h,bots", BOUNDARY)
 def test_gpu_lockstep_boundary_shapes(tmp_path, w, h, bots, partial_obs):
     """HIP == oracle every tick on the largest accepted shapes: 150 units on a random map,
-    masked + unmasked agent actions, 200 ticks with max_steps 90 (auto-resets inside)."""
+    masked + unmasked agent actions, 200 ticks with max_steps 90 (auto-resets inside); the
+    k_bot arm on the tensor path with float32 obs, compared as bits."""
     from test_gpu_bots import BOTS, lockstep
 
     p = write_random_map(str(tmp_path / f"g{w}x{h}.xml"), w, h, 7, n_units=150, wall_frac=0.1)
     ais = (BOTS + ["passiveAI"]) if bots else []
     lockstep(ais, p, 4, 200, partial_obs=partial_obs, seed=w * 100 + h, max_steps=90, mode="mixed")
     if bots:   # the same with the bots in their own kernel (k_bot) instead of fused into the step
-        lockstep(ais, p, 2, 120, partial_obs=partial_obs, seed=h, max_steps=60, bot_fusion=False)
+        lockstep(ais, p, 2, 120, partial_obs=partial_obs, seed=h, max_steps=60, bot_fusion=False, return_tensors=True,
+                 obs_dtype="float32")
 
 
 @pytest.mark.gpu

@@ -131,9 +131,11 @@ def test_campaign_maps_load_in_both_loaders(tmp_path):
 @pytest.mark.parametrize("k", range(NCAMP))
 def test_gpu_lockstep_pcg_campaign(tmp_path, k):
     """Campaign map k: 4 selfplay envs + coacAI / workerRushAI / lightRushAI / randomBiasedAI,
-    300 ticks, max_steps 120, fog on odd k: HIP == oracle every tick."""
+    300 ticks, max_steps 120, fog on odd k, the tensor path with float32 obs (the bench's
+    dtype, compared as bits) on k % 4 >= 2: HIP == oracle every tick."""
     from test_gpu_bots import lockstep
 
     p, m = _campaign_map(tmp_path, k)
+    f32 = dict(return_tensors=True, obs_dtype="float32") if k % 4 >= 2 else {}
     lockstep(["coacAI", "workerRushAI", "lightRushAI", "randomBiasedAI"], p, 4, 300, partial_obs=bool(k % 2), seed=k,
-             max_steps=120)
+             max_steps=120, **f32)
