@@ -127,7 +127,8 @@ def test_fuzz_checkpoint_replays_bit_for_bit(tmp_path, seed):
     """Random maps (tests/random_maps.py, 4..32 x 4..32, walls), random device bots
     (randomBiasedAI's tick-keyed stream included), selfplay, fog, map cycling over two random
     maps of one size, short time limits: the snapshot taken at a random tick replays a random
-    continuation bit for bit (MRTS_FUZZ_SEEDS // 3 cases)."""
+    continuation bit for bit (MRTS_FUZZ_SEEDS // 3 cases); odd seeds on float32 obs (the bench's
+    dtype), even seeds on int32."""
     import torch
 
     from gym_microrts import microrts_ai
@@ -146,7 +147,7 @@ def test_fuzz_checkpoint_replays_bit_for_bit(tmp_path, seed):
     env = MicroRTSGridModeVecEnv(num_selfplay_envs=nsp, num_bot_envs=len(bots), max_steps=int(rng.integers(20, 80)),
                                  ai2s=[getattr(microrts_ai, b) for b in bots], map_paths=[maps[0]],
                                  partial_obs=bool(rng.integers(0, 2)), reward_weight=W, return_tensors=True,
-                                 obs_dtype=torch.int32, bot_fusion=bool(rng.integers(0, 4)), **kw)
+                                 obs_dtype=torch.float32 if seed % 2 else torch.int32, bot_fusion=bool(rng.integers(0, 4)), **kw)
     env.reset()
     act = torch.empty((env.num_envs, env.height * env.width, 7), dtype=torch.int64, device=env.device)
     t0, t1 = int(rng.integers(0, 120)), int(rng.integers(1, 120))
